@@ -1,0 +1,195 @@
+/*
+ * crt_hip.h — C ABI of the MI355X (gfx950) render layer: libcrt_hip.so.
+ *
+ * This is the drop-in boundary for the reference's device path
+ * (Mordentary/RayTracer-Cuda, paths relative to CudaRayTracer/src/):
+ *
+ *   reference                                            replaced by
+ *   ---------------------------------------------------  ------------------------------------
+ *   CUDARenderer::initialize  (CUDARenderer.cuh:39-49)   crt_renderer_create + crt_renderer_init_rand
+ *     initRandState<<<>>>     (CUDAKernels.h:18-26)      crt_renderer_init_rand
+ *   CUDARenderer::updateCamera (CUDARenderer.cuh:51-53)  crt_renderer_set_camera
+ *     cudaMemcpyToSymbol(d_camera) (Camera.cuh:213)
+ *   CUDARenderer::render      (CUDARenderer.cuh:55-60)   crt_renderer_render + crt_renderer_resolve
+ *     render<<<>>> / rayColor (CUDAKernels.h:102-166)    (crt_renderer_render_frame does both)
+ *   CUDARenderer::getImageData (CUDARenderer.cuh:16)     crt_renderer_rgba_device_ptr / _read_rgba8
+ *   CUDARenderer::getRandState (CUDARenderer.cuh:17)     crt_renderer_rng_device_ptr
+ *   SceneManager::initializeScene device half           crt_scene_create (flat arrays; the host
+ *     createRandomWorld / initMesh / createBVH <<<1,1>>>   builds the BVHs with the reference's
+ *     (CUDAKernels.h:28-100, SceneManager.h:77-98)         semantics, see crt_host.h)
+ *   SceneManager::getBVHNodes / getWorld (SceneManager.h:25-26)  the crt_scene handle
+ *   CUDA_CHECK -> throw (CUDAHelpers.h:19-26)            int status + crt_last_error()
+ *
+ * Plain C: pointers and sizes only.  All device memory is owned by the opaque
+ * handles; the caller owns every host buffer.  Handles are not thread-safe; use
+ * one renderer per device (one process per GPU for multi-GPU).
+ */
+#ifndef CRT_HIP_H
+#define CRT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRT_ABI_VERSION 1
+
+enum crt_status {
+    CRT_OK = 0,
+    CRT_ERR_INVALID_ARGUMENT = -1,
+    CRT_ERR_HIP = -2,          /* a HIP runtime call failed; see crt_last_error() */
+    CRT_ERR_OUT_OF_MEMORY = -3,
+    CRT_ERR_NO_DEVICE = -4,
+    CRT_ERR_UNSUPPORTED = -5
+};
+
+/* Material.cuh:8-14 MaterialType */
+enum crt_material_type { CRT_LAMBERTIAN = 0, CRT_METAL = 1, CRT_DIELECTRIC = 2, CRT_DIFFUSE_LIGHT = 3 };
+
+/* Material.cuh:16-47 MaterialData (roughness is clamped to <= 1 like the Metal ctor, Material.cuh:86). */
+typedef struct crt_material_desc {
+    int32_t type;
+    float albedo[3];
+    float emission[3];
+    float roughness;
+    float ior;
+} crt_material_desc;
+
+/* One reference BVHNode (BVHNode.cuh:347-354 fields): box + children / leaf range. */
+typedef struct crt_bvh_node_desc {
+    float bmin[3];
+    float bmax[3];
+    int32_t left, right;          /* internal nodes */
+    int32_t obj_index, obj_count; /* leaves: mesh = index range [obj_index, obj_index+obj_count) step 3;
+                                     scene = object index */
+    int32_t is_leaf;
+} crt_bvh_node_desc;
+
+/* One Mesh (Mesh.cuh:18-53 ctor arguments + its built BVH). */
+typedef struct crt_mesh_desc {
+    uint32_t vertex_offset, vertex_count;
+    uint32_t index_offset, index_count;
+    uint32_t face_offset;          /* into face_materials */
+    uint32_t material_id_offset;   /* Mesh::m_MatIDOffset */
+    const crt_bvh_node_desc* nodes;/* Mesh::m_MeshBVH in builder index order (root = 0) */
+    int32_t node_count;
+    float aabb[6];                 /* Mesh::m_BoundingBox  min xyz, max xyz */
+} crt_mesh_desc;
+
+/* Sphere.cuh:20-25 */
+typedef struct crt_sphere_desc {
+    float center[3];
+    float radius;
+    int32_t material;
+} crt_sphere_desc;
+
+enum crt_object_kind { CRT_OBJECT_MESH = 0, CRT_OBJECT_SPHERE = 1 };
+typedef struct crt_object_desc {   /* HittableList::m_Objects entry (HittableList.cuh:331) */
+    int32_t kind;
+    int32_t index;                 /* into meshes[] or spheres[] */
+} crt_object_desc;
+
+typedef struct crt_scene_desc {
+    const float* positions;        /* vertex slots, xyz per slot (Vertex::Position, Mesh.cuh:5-10) */
+    uint64_t n_positions;
+    const uint32_t* indices;       /* per-mesh local vertex indices, AFTER the mesh BVH build permuted them */
+    uint64_t n_indices;
+    const int32_t* face_materials; /* per triangle, permuted with the indices */
+    uint64_t n_faces;
+    const crt_mesh_desc* meshes;
+    int32_t n_meshes;
+    const crt_sphere_desc* spheres;
+    int32_t n_spheres;
+    const crt_object_desc* objects;   /* HittableList order (CUDAKernels.h:64-73) */
+    int32_t n_objects;
+    const crt_bvh_node_desc* scene_nodes;  /* BVHNode::buildBVHScene output, root = 0 */
+    int32_t n_scene_nodes;
+    const crt_material_desc* materials;    /* HittableList::m_Materials order */
+    int32_t n_materials;
+} crt_scene_desc;
+
+/* Camera POD as the kernel needs it (Camera.cuh:32-44 reads exactly these). */
+typedef struct crt_camera_desc {
+    float origin[3];       /* m_Position */
+    float lower_left[3];   /* m_LowerLeftCorner */
+    float horizontal[3];   /* m_Horizontal */
+    float vertical[3];     /* m_Vertical */
+    float right[3];        /* m_Right */
+    float up[3];           /* m_Up */
+    float lens_radius;     /* m_LensRadius */
+    int32_t samples_per_pixel;   /* m_SamplesPerPixel */
+    float pixel_sample_scale;    /* m_PixelSampleScale = 1.f / spp */
+} crt_camera_desc;
+
+typedef struct crt_scene_stats {
+    int64_t device_nodes;      /* flattened (threaded, DFS-preorder) nodes incl. scene level */
+    int64_t device_prims;      /* triangles + spheres */
+    int64_t device_bytes;      /* node + prim + material bytes resident in HBM */
+    int32_t max_depth;         /* deepest node (scene + mesh levels) */
+    int32_t n_materials;
+} crt_scene_stats;
+
+typedef struct crt_work_counters {  /* filled by a CRT_RENDER_COUNT_WORK render */
+    uint64_t rays;           /* closest-hit queries = calls of the scene-level hit (CUDAKernels.h:123) */
+    uint64_t box_tests;      /* AABB::hit calls (scene + mesh levels) */
+    uint64_t tri_tests;      /* rayTriangleIntersect calls */
+    uint64_t sphere_tests;   /* Sphere::hit calls */
+    uint64_t paths;          /* samples completed */
+} crt_work_counters;
+
+/* render flags */
+#define CRT_RENDER_ACCUMULATE  1u   /* add into the existing linear sum instead of starting from 0 */
+#define CRT_RENDER_COUNT_WORK  2u   /* counting kernel variant: fills crt_work_counters (slower) */
+
+typedef struct crt_scene crt_scene;
+typedef struct crt_renderer crt_renderer;
+
+int crt_abi_version(void);
+const char* crt_last_error(void);   /* thread-local message of the last failing call */
+int crt_device_count(int* out);
+
+/* ---- scene (SceneManager device half) ---- */
+int  crt_scene_create(const crt_scene_desc* desc, int device, crt_scene** out);
+int  crt_scene_get_stats(const crt_scene* scene, crt_scene_stats* out);
+void crt_scene_destroy(crt_scene* scene);
+
+/* ---- renderer (CUDARenderer) ---- */
+int  crt_renderer_create(int width, int height, int device, crt_renderer** out);
+void crt_renderer_destroy(crt_renderer* r);
+/* curand_init(seed, subsequence_base + y*width + x, 0) per pixel (CUDAKernels.h:18-26).
+ * subsequence_base = shard * width * height for spp sharding. */
+int  crt_renderer_init_rand(crt_renderer* r, unsigned long long seed, unsigned long long subsequence_base, void* stream);
+int  crt_renderer_set_camera(crt_renderer* r, const crt_camera_desc* cam);
+/* Trace `spp` samples per pixel continuing each pixel's RNG stream; the per-pixel
+ * linear sum (pixel_color, CUDAKernels.h:157-162) is kept in an fp32 W*H*3 buffer. */
+int  crt_renderer_render(crt_renderer* r, const crt_scene* scene, int spp, int max_bounces, unsigned flags, void* stream);
+/* RGBA8 = writeColor(scale * sum) (CRTUtility.cuh:14-32); row 0 is the bottom row. */
+int  crt_renderer_resolve(crt_renderer* r, float scale, void* stream);
+/* The reference's CUDARenderer::render: fresh sum, camera spp, 20 bounces, resolve, synchronize. */
+int  crt_renderer_render_frame(crt_renderer* r, const crt_scene* scene, void* stream);
+int  crt_renderer_synchronize(crt_renderer* r, void* stream);
+int  crt_renderer_read_linear(crt_renderer* r, float* host_out);        /* W*H*3 floats */
+int  crt_renderer_read_rgba8(crt_renderer* r, uint8_t* host_out);        /* W*H*4 bytes */
+int  crt_renderer_read_rng(crt_renderer* r, uint32_t* host_out);         /* W*H*6 words: v[5], d */
+int  crt_renderer_write_linear(crt_renderer* r, const float* host_in);  /* e.g. after a host-side reduce */
+int  crt_renderer_get_counters(crt_renderer* r, crt_work_counters* out);/* of the last render call */
+float* crt_renderer_linear_device_ptr(crt_renderer* r);   /* for RCCL reduce of the framebuffer */
+uint8_t* crt_renderer_rgba_device_ptr(crt_renderer* r);
+uint32_t* crt_renderer_rng_device_ptr(crt_renderer* r);
+/* Milliseconds of the last render kernel launch(es), measured with HIP events on the launch stream. */
+float crt_renderer_last_kernel_ms(crt_renderer* r);
+
+/* ---- self-test of the arithmetic the kernel depends on (IEEE f32/f64 div/sqrt) ---- */
+/* For n inputs a[i], b[i] (f32) computes on the device: a/b, sqrtf(|a|), 1/a, (double)sqrt((double)|a|)
+ * into out[4*i..4*i+3] (the last one converted to float bits as a double->float cast). */
+int crt_selftest_math(const float* a, const float* b, int n, float* out, double* out_f64);
+/* XORWOW device self-test: init(seed, subseq[i]) then n_draw uniforms per entry. */
+int crt_selftest_rng(unsigned long long seed, const unsigned long long* subseq, int n, int n_draw,
+                     uint32_t* state_out /* n*6 */, float* uniforms_out /* n*n_draw */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CRT_HIP_H */

@@ -1,0 +1,222 @@
+"""crt_amd — Python front-end of the MI355X path tracer.
+
+Mirrors the reference's host API for the render path (CudaRayTracer/src):
+  HostScene      ~ SceneManager host half (OBJ load, normalisation, BVH builds; C++ libcrt_host.so)
+  Scene          ~ the device scene (SceneManager::getBVHNodes()/getWorld(); libcrt_hip.so)
+  Renderer       ~ CUDARenderer (initialize / updateCamera / render / getImageData)
+  camera(...)    ~ CRT::Camera(aspect, fov, position, target, up, aperture, focus)
+All compute runs in the HIP library; nothing here computes pixels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import CameraDesc, CrtError, SceneDesc, SceneStats, WorkCounters, build, check, check_host
+
+RENDER_ACCUMULATE = 1
+RENDER_COUNT_WORK = 2
+
+# The screenshot-reproducing bench pose: the reference's default pose
+# (Raytracer.h:77-82, pos (0,4,4), target ignored) does not frame the box.
+BENCH_CAMERA = dict(aspect=16.0 / 9.0, vfov=80.0, pos=(0.0, 0.0, 0.3), up=(0.0, 1.0, 0.0),
+                    aperture=0.000001, focus=0.3, yaw=-90.0, pitch=0.0)
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def camera(spp: int = 1, aspect=16.0 / 9.0, vfov=80.0, pos=(0.0, 0.0, 0.3), up=(0.0, 1.0, 0.0),
+           aperture=0.000001, focus=0.3, yaw=-90.0, pitch=0.0) -> CameraDesc:
+    """CRT::Camera (Camera.cuh:18-30, :159-182) computed by the C++ host library."""
+    d = CameraDesc()
+    check_host(_lib.host().crth_camera(C.c_float(aspect), C.c_float(vfov), _p(np.asarray(pos, np.float32)),
+                                       _p(np.asarray(up, np.float32)), C.c_float(aperture), C.c_float(focus),
+                                       C.c_float(yaw), C.c_float(pitch), int(spp), C.byref(d)), "crth_camera")
+    return d
+
+
+def camera_floats(d: CameraDesc) -> np.ndarray:
+    """19-float layout shared with the oracle (origin, llc, horizontal, vertical, right, up, lens_radius)."""
+    return np.array(list(d.origin) + list(d.lower_left) + list(d.horizontal) + list(d.vertical) +
+                    list(d.right) + list(d.up) + [d.lens_radius], dtype=np.float32)
+
+
+class HostScene:
+    """SceneManager host half: load OBJ files, normalise, build mesh + scene BVHs (C++)."""
+
+    def __init__(self, obj_files):
+        files = [str(f) for f in obj_files]
+        arr = (C.c_char_p * len(files))(*[f.encode() for f in files])
+        h = C.c_void_p()
+        check_host(_lib.host().crth_scene_load(arr, len(files), C.byref(h)), "crth_scene_load")
+        self.h = h
+        self.files = files
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            _lib.host().crth_scene_destroy(self.h)
+            self.h = None
+
+    def counts(self):
+        c = np.zeros(5, np.int64)
+        check_host(_lib.host().crth_scene_counts(self.h, _p(c)), "crth_scene_counts")
+        return dict(n_meshes=int(c[0]), n_slots=int(c[1]), n_indices=int(c[2]), n_faces=int(c[3]),
+                    n_materials=int(c[4]))
+
+    def loader_arrays(self):
+        c = self.counts()
+        pos = np.zeros((c["n_slots"], 3), np.float32)
+        idx = np.zeros(c["n_indices"], np.uint32)
+        fm = np.zeros(c["n_faces"], np.int32)
+        info = np.zeros((c["n_meshes"], 6), np.uint32)
+        mats = np.zeros((c["n_materials"], 9), np.float32)
+        check_host(_lib.host().crth_scene_loader_arrays(self.h, _p(pos), _p(idx), _p(fm), _p(info), _p(mats)),
+                   "crth_scene_loader_arrays")
+        return pos, idx, fm, info, mats
+
+    def desc(self) -> SceneDesc:
+        d = SceneDesc()
+        check_host(_lib.host().crth_scene_desc(self.h, C.byref(d)), "crth_scene_desc")
+        return d
+
+    def mesh_bvh(self, i: int):
+        """(boxes[n,6], ints[n,5] = left,right,obj_index,obj_count,is_leaf) in builder index order."""
+        d = self.desc()
+        meshes = C.cast(d.meshes, C.POINTER(_lib.MeshDesc))
+        m = meshes[i]
+        return _nodes_to_np(m.nodes, m.node_count), np.array(m.aabb, np.float32)
+
+    def scene_bvh(self):
+        d = self.desc()
+        return _nodes_to_np(d.scene_nodes, d.n_scene_nodes)
+
+    def permuted(self):
+        d = self.desc()
+        idx = np.ctypeslib.as_array(C.cast(d.indices, C.POINTER(C.c_uint32)), (d.n_indices,)).copy()
+        fm = np.ctypeslib.as_array(C.cast(d.face_materials, C.POINTER(C.c_int32)), (d.n_faces,)).copy()
+        return idx, fm
+
+    def upload(self, device: int = 0) -> "Scene":
+        h = C.c_void_p()
+        check_host(_lib.host().crth_scene_upload(self.h, int(device), C.byref(h)), "crth_scene_upload")
+        return Scene(h, device)
+
+
+def _nodes_to_np(ptr, n):
+    if n == 0:
+        return np.zeros((0, 6), np.float32), np.zeros((0, 5), np.int32)
+    raw = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), (n * C.sizeof(_lib.BvhNodeDesc),))
+    rec = raw.view(np.dtype([("b", "<f4", 6), ("i", "<i4", 5)]))
+    return rec["b"].copy(), rec["i"].copy()
+
+
+class Scene:
+    """Device scene handle (crt_scene)."""
+
+    def __init__(self, handle, device):
+        self.h = handle
+        self.device = device
+
+    def stats(self) -> dict:
+        s = SceneStats()
+        check(_lib.hip().crt_scene_get_stats(self.h, C.byref(s)), "crt_scene_get_stats")
+        return {k: getattr(s, k) for k, _ in SceneStats._fields_}
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.hip().crt_scene_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+
+def load_scene(obj_files, device: int = 0):
+    hs = HostScene(obj_files)
+    return hs, hs.upload(device)
+
+
+class Renderer:
+    """CUDARenderer equivalent over crt_renderer (CUDARenderer.cuh:9-60)."""
+
+    def __init__(self, width: int, height: int, device: int = 0):
+        h = C.c_void_p()
+        check(_lib.hip().crt_renderer_create(int(width), int(height), int(device), C.byref(h)), "crt_renderer_create")
+        self.h, self.width, self.height, self.device = h, width, height, device
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.hip().crt_renderer_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def init_rand(self, seed: int = 41, subsequence_base: int = 0, stream=None):
+        check(_lib.hip().crt_renderer_init_rand(self.h, int(seed), int(subsequence_base), stream), "init_rand")
+
+    def set_camera(self, cam: CameraDesc):
+        self._cam = cam
+        check(_lib.hip().crt_renderer_set_camera(self.h, C.byref(cam)), "set_camera")
+
+    def render(self, scene: Scene, spp: int, max_bounces: int = 20, accumulate=False, count_work=False, stream=None):
+        flags = (RENDER_ACCUMULATE if accumulate else 0) | (RENDER_COUNT_WORK if count_work else 0)
+        check(_lib.hip().crt_renderer_render(self.h, scene.h, int(spp), int(max_bounces), flags, stream), "render")
+
+    def resolve(self, scale: float, stream=None):
+        check(_lib.hip().crt_renderer_resolve(self.h, C.c_float(scale), stream), "resolve")
+
+    def synchronize(self, stream=None):
+        check(_lib.hip().crt_renderer_synchronize(self.h, stream), "synchronize")
+
+    def linear(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 3), np.float32)
+        check(_lib.hip().crt_renderer_read_linear(self.h, _p(out)), "read_linear")
+        return out
+
+    def write_linear(self, arr: np.ndarray):
+        a = np.ascontiguousarray(arr, np.float32)
+        check(_lib.hip().crt_renderer_write_linear(self.h, _p(a)), "write_linear")
+
+    def rgba8(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 4), np.uint8)
+        check(_lib.hip().crt_renderer_read_rgba8(self.h, _p(out)), "read_rgba8")
+        return out
+
+    def rng_state(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 6), np.uint32)
+        check(_lib.hip().crt_renderer_read_rng(self.h, _p(out)), "read_rng")
+        return out
+
+    def counters(self) -> dict:
+        w = WorkCounters()
+        check(_lib.hip().crt_renderer_get_counters(self.h, C.byref(w)), "get_counters")
+        return {k: int(getattr(w, k)) for k, _ in WorkCounters._fields_}
+
+    def last_kernel_ms(self) -> float:
+        return float(_lib.hip().crt_renderer_last_kernel_ms(self.h))
+
+    def linear_device_ptr(self) -> int:
+        return int(_lib.hip().crt_renderer_linear_device_ptr(self.h) or 0)
+
+    def render_frame(self, scene: Scene, spp: int, max_bounces: int = 20, seed: int = 41, subsequence_base: int = 0,
+                     stream=None):
+        """Fresh RNG (initRandState) + spp samples + writeColor: one reference frame."""
+        self.init_rand(seed, subsequence_base, stream)
+        self.render(scene, spp, max_bounces, stream=stream)
+        self.resolve(pixel_sample_scale(spp), stream)
+        self.synchronize(stream)
+
+
+def pixel_sample_scale(spp: int) -> float:
+    """m_PixelSampleScale = 1.f / m_SamplesPerPixel (Camera.cuh:23), rounded to f32."""
+    return float(np.float32(1.0) / np.float32(spp))
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(_lib.hip().crt_device_count(C.byref(n)), "device_count")
+    return n.value

@@ -1,0 +1,149 @@
+"""ctypes bindings of the two C ABIs (include/crt_hip.h, include/crt_host.h).
+
+The shared libraries are built in-tree (raytracer-cuda_amd/lib/) by `make`; this
+module never falls back to anything else: if libcrt_hip.so is missing or does not
+load, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+PKG_ROOT = Path(__file__).resolve().parents[1]          # raytracer-cuda_amd/
+REPO = PKG_ROOT.parent
+LIB_DIR = PKG_ROOT / "lib"
+HIP_LIB = LIB_DIR / "libcrt_hip.so"
+HOST_LIB = LIB_DIR / "libcrt_host.so"
+
+
+class CrtError(RuntimeError):
+    pass
+
+
+def build(jobs: int = 8) -> None:
+    """Compile libcrt_hip.so (gfx950) + libcrt_host.so + crt_render in-tree."""
+    subprocess.run(["make", "-C", str(PKG_ROOT), f"-j{jobs}", "all"], check=True)
+
+
+class CameraDesc(C.Structure):
+    _fields_ = [("origin", C.c_float * 3), ("lower_left", C.c_float * 3), ("horizontal", C.c_float * 3),
+                ("vertical", C.c_float * 3), ("right", C.c_float * 3), ("up", C.c_float * 3),
+                ("lens_radius", C.c_float), ("samples_per_pixel", C.c_int32), ("pixel_sample_scale", C.c_float)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("positions", C.c_void_p), ("n_positions", C.c_uint64), ("indices", C.c_void_p),
+                ("n_indices", C.c_uint64), ("face_materials", C.c_void_p), ("n_faces", C.c_uint64),
+                ("meshes", C.c_void_p), ("n_meshes", C.c_int32), ("spheres", C.c_void_p), ("n_spheres", C.c_int32),
+                ("objects", C.c_void_p), ("n_objects", C.c_int32), ("scene_nodes", C.c_void_p),
+                ("n_scene_nodes", C.c_int32), ("materials", C.c_void_p), ("n_materials", C.c_int32)]
+
+
+class BvhNodeDesc(C.Structure):
+    _fields_ = [("bmin", C.c_float * 3), ("bmax", C.c_float * 3), ("left", C.c_int32), ("right", C.c_int32),
+                ("obj_index", C.c_int32), ("obj_count", C.c_int32), ("is_leaf", C.c_int32)]
+
+
+class MeshDesc(C.Structure):
+    _fields_ = [("vertex_offset", C.c_uint32), ("vertex_count", C.c_uint32), ("index_offset", C.c_uint32),
+                ("index_count", C.c_uint32), ("face_offset", C.c_uint32), ("material_id_offset", C.c_uint32),
+                ("nodes", C.c_void_p), ("node_count", C.c_int32), ("aabb", C.c_float * 6)]
+
+
+class SceneStats(C.Structure):
+    _fields_ = [("device_nodes", C.c_int64), ("device_prims", C.c_int64), ("device_bytes", C.c_int64),
+                ("max_depth", C.c_int32), ("n_materials", C.c_int32)]
+
+
+class WorkCounters(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("box_tests", C.c_uint64), ("tri_tests", C.c_uint64),
+                ("sphere_tests", C.c_uint64), ("paths", C.c_uint64)]
+
+
+# exported symbol lists (checked by tests against include/*.h)
+HIP_SYMBOLS = [
+    "crt_abi_version", "crt_last_error", "crt_device_count", "crt_scene_create", "crt_scene_get_stats",
+    "crt_scene_destroy", "crt_renderer_create", "crt_renderer_destroy", "crt_renderer_init_rand",
+    "crt_renderer_set_camera", "crt_renderer_render", "crt_renderer_resolve", "crt_renderer_render_frame",
+    "crt_renderer_synchronize", "crt_renderer_read_linear", "crt_renderer_read_rgba8", "crt_renderer_read_rng",
+    "crt_renderer_write_linear", "crt_renderer_get_counters", "crt_renderer_linear_device_ptr",
+    "crt_renderer_rgba_device_ptr", "crt_renderer_rng_device_ptr", "crt_renderer_last_kernel_ms",
+    "crt_selftest_math", "crt_selftest_rng",
+]
+HOST_SYMBOLS = [
+    "crth_scene_load", "crth_scene_destroy", "crth_scene_desc", "crth_scene_upload", "crth_scene_counts",
+    "crth_scene_loader_arrays", "crth_camera", "crth_last_error",
+]
+
+_hip = None
+_host = None
+
+
+def hip():
+    global _hip
+    if _hip is None:
+        if not HIP_LIB.exists():
+            raise CrtError(f"{HIP_LIB} not built (run `make -C {PKG_ROOT}` or __graft_entry__.build())")
+        L = C.CDLL(str(HIP_LIB), mode=C.RTLD_GLOBAL)
+        P, i32, u64, f32 = C.c_void_p, C.c_int, C.c_ulonglong, C.c_float
+        sig = {
+            "crt_abi_version": ([], i32), "crt_last_error": ([], C.c_char_p),
+            "crt_device_count": ([P], i32),
+            "crt_scene_create": ([P, i32, P], i32), "crt_scene_get_stats": ([P, P], i32),
+            "crt_scene_destroy": ([P], None),
+            "crt_renderer_create": ([i32, i32, i32, P], i32), "crt_renderer_destroy": ([P], None),
+            "crt_renderer_init_rand": ([P, u64, u64, P], i32), "crt_renderer_set_camera": ([P, P], i32),
+            "crt_renderer_render": ([P, P, i32, i32, C.c_uint, P], i32),
+            "crt_renderer_resolve": ([P, f32, P], i32), "crt_renderer_render_frame": ([P, P, P], i32),
+            "crt_renderer_synchronize": ([P, P], i32),
+            "crt_renderer_read_linear": ([P, P], i32), "crt_renderer_read_rgba8": ([P, P], i32),
+            "crt_renderer_read_rng": ([P, P], i32), "crt_renderer_write_linear": ([P, P], i32),
+            "crt_renderer_get_counters": ([P, P], i32),
+            "crt_renderer_linear_device_ptr": ([P], P), "crt_renderer_rgba_device_ptr": ([P], P),
+            "crt_renderer_rng_device_ptr": ([P], P), "crt_renderer_last_kernel_ms": ([P], f32),
+            "crt_selftest_math": ([P, P, i32, P, P], i32),
+            "crt_selftest_rng": ([u64, P, i32, i32, P, P], i32),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _hip = L
+    return _hip
+
+
+def host():
+    global _host
+    if _host is None:
+        hip()   # load libcrt_hip.so first (RTLD_GLOBAL) so libcrt_host resolves against the in-tree copy
+        if not HOST_LIB.exists():
+            raise CrtError(f"{HOST_LIB} not built")
+        L = C.CDLL(str(HOST_LIB))
+        P, i32, f32 = C.c_void_p, C.c_int, C.c_float
+        sig = {
+            "crth_scene_load": ([P, i32, P], i32), "crth_scene_destroy": ([P], None),
+            "crth_scene_desc": ([P, P], i32), "crth_scene_upload": ([P, i32, P], i32),
+            "crth_scene_counts": ([P, P], i32), "crth_scene_loader_arrays": ([P, P, P, P, P, P], i32),
+            "crth_camera": ([f32, f32, P, P, f32, f32, f32, f32, i32, P], i32),
+            "crth_last_error": ([], C.c_char_p),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _host = L
+    return _host
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = hip().crt_last_error().decode(errors="replace")
+        raise CrtError(f"{what} failed (status {rc}): {msg}")
+
+
+def check_host(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = host().crth_last_error().decode(errors="replace")
+        raise CrtError(f"{what} failed (status {rc}): {msg}")

@@ -1,0 +1,116 @@
+// crt_device.h — device-side building blocks of the gfx950 render kernel.
+//
+// Every function restates one reference function with the SAME floating-point
+// operation order (no contraction: the library is built with -ffp-contract=off,
+// IEEE f32/f64 division and sqrt), so the HIP path is bit-identical to the
+// reference's arithmetic.  Reference paths are relative to CudaRayTracer/src/.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace crt {
+
+// ---------------------------------------------------------------- layout
+// Flattened scene in HBM (built by crt_hip.hip from the host-built reference BVHs):
+//
+// nodes: 2 x float4 (32 B) per node, DFS preorder over the scene BVH with every
+// mesh BVH spliced in after its scene leaf ("threaded" BVH: left child = next
+// node, `skip` = first node after the subtree).  The left-first stack DFS of
+// BVHNode::hit (BVHNode.cuh:304-345) and Mesh::hit (Mesh.cuh:55-110) visits
+// exactly this order, so the traversal needs no stack at all.
+//   A = (min.x, min.y, min.z, max.x)   B = (max.y, max.z, a, b)
+//   internal mesh node : a = skip, b = NODE_MESH_INNER  (box tested against [0.001, closest])
+//   scene node / scene mesh leaf : a = skip, b = NODE_SCENE_INNER (box tested against [0.001, inf),
+//                                   the unshrunk ray_t of BVHNode::hit, BVHNode.cuh:318)
+//   mesh leaf          : a = triangle count, b = first triangle prim (>= 0)
+//   sphere leaf        : a = 0, b = SPHERE_BIT | sphere prim          (scene level: [0.001, inf))
+//   every leaf continues at node + 1.
+// prims: 3 x float4 (48 B) per primitive.
+//   triangle: (v0.xyz, e1.x) (e1.y, e1.z, e2.xy) (e2.z, material, 0, 0)   e1 = v1-v0, e2 = v2-v0
+//             (bit-identical to Mesh.cuh:277-278, which subtracts in f32 too)
+//   sphere  : (center.xyz, radius) (radius^2, material, 0, 0) (0,0,0,0)
+// materials: 3 x float4 (48 B): (type, albedo.xyz) (emission.xyz, roughness) (ior, 0, 0, 0)
+constexpr int NODE_MESH_INNER = -1;
+constexpr int NODE_SCENE_INNER = -3;
+constexpr int SPHERE_BIT = 1 << 30;
+
+struct V3 { float x, y, z; };
+
+__device__ __forceinline__ V3 v3(float a, float b, float c) { return V3{a, b, c}; }
+__device__ __forceinline__ V3 operator+(V3 u, V3 v) { return v3(u.x + v.x, u.y + v.y, u.z + v.z); }   // Vec3.cuh:173
+__device__ __forceinline__ V3 operator-(V3 u, V3 v) { return v3(u.x - v.x, u.y - v.y, u.z - v.z); }   // :177
+__device__ __forceinline__ V3 operator*(V3 u, V3 v) { return v3(u.x * v.x, u.y * v.y, u.z * v.z); }   // :181
+__device__ __forceinline__ V3 operator*(float t, V3 v) { return v3(t * v.x, t * v.y, t * v.z); }      // :185
+__device__ __forceinline__ V3 operator-(V3 v) { return v3(-v.x, -v.y, -v.z); }                       // :21
+__device__ __forceinline__ float dot(V3 u, V3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }       // :216
+__device__ __forceinline__ V3 cross(V3 u, V3 v) {                                                     // :220
+    return v3(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
+}
+__device__ __forceinline__ float len2(V3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }            // :95
+__device__ __forceinline__ V3 unit(V3 v) { return (1.0f / sqrtf(len2(v))) * v; }                     // :201,:213
+__device__ __forceinline__ V3 reflect(V3 v, V3 n) { return v - (2.0f * dot(v, n)) * n; }              // :225
+__device__ __forceinline__ V3 refract(V3 uv, V3 n, float eta) {                                        // :229
+    float cos_theta = fminf(dot(-uv, n), 1.0f);
+    V3 perp = eta * (uv + cos_theta * n);
+    V3 par = (-sqrtf(fabsf(1.0f - len2(perp)))) * n;
+    return perp + par;
+}
+
+// ------------------------------------------------------------------ XORWOW
+// cuRAND XORWOW (CUDA 12.5 curand_kernel.h: curand, _curand_uniform) — see DESIGN.md.
+struct Rng { uint32_t v0, v1, v2, v3, v4, d; };
+
+__device__ __forceinline__ uint32_t next_u32(Rng& s) {
+    uint32_t t = s.v0 ^ (s.v0 >> 2);
+    s.v0 = s.v1; s.v1 = s.v2; s.v2 = s.v3; s.v3 = s.v4;
+    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+    s.d += 362437u;
+    return s.v4 + s.d;
+}
+__device__ __forceinline__ float uniform(Rng& s) {
+    const float inv = 2.3283064e-10f;   // CURAND_2POW32_INV
+    return (float)next_u32(s) * inv + (inv / 2.0f);
+}
+// Utility.cuh:168-171: min + (max - min) * U, here min=-1, max=1.
+__device__ __forceinline__ float rand_pm1(Rng& s) { return -1.0f + 2.0f * uniform(s); }
+
+__device__ __forceinline__ V3 rand_unit_vector(Rng& s) {   // Utility.cuh:195-203, :223-226
+    V3 p;
+    for (;;) {
+        float a = rand_pm1(s);
+        float b = rand_pm1(s);
+        float c = rand_pm1(s);
+        p = v3(a, b, c);
+        if (len2(p) >= 1) continue;
+        break;
+    }
+    return unit(p);
+}
+
+// Material.cuh:132-137 with pow(float,int) restated as exponentiation by squaring.
+__device__ __forceinline__ float schlick(float cosine, float ref_idx) {
+    float r0 = (1 - ref_idx) / (1 + ref_idx);
+    r0 = r0 * r0;
+    float a = 1 - cosine;
+    float r = 1.0f * a;          // e = 5: bit0
+    a = a * a;                   // e = 2
+    a = a * a;                   // e = 1
+    r = r * a;
+    return r0 + (1 - r0) * r;
+}
+
+__device__ __forceinline__ V3 sky(V3 d) {   // CRTUtility.cuh:34-38
+    V3 ud = unit(d);
+    float t = 0.5f * (ud.y + 1.0f);
+    return (1.0f - t) * v3(1.0f, 1.0f, 1.0f) + t * v3(0.5f, 0.7f, 1.0f);
+}
+
+__device__ __forceinline__ unsigned char to_u8(float c) {   // CRTUtility.cuh:14-32
+    double x = c;
+    float g = (float)(x > 0 ? sqrt(x) : 0);
+    if (g < 0.000f) g = 0.000f;
+    else if (g > 0.999f) g = 0.999f;
+    return (unsigned char)(256 * g);
+}
+
+}  // namespace crt

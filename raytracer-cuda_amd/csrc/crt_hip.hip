@@ -1,0 +1,838 @@
+// crt_hip.hip — MI355X (gfx950) render layer: kernels + the C ABI of include/crt_hip.h.
+//
+// Hot path: crt_render_kernel — one lane per pixel (8x8 pixel tile per wave64,
+// 16x16 per 256-thread workgroup), the pixel's samples traced strictly in order
+// so each pixel's XORWOW stream is consumed exactly as in the reference
+// (CUDAKernels.h:147-166).  Inside a wave, lanes are decoupled at PATH-SEGMENT
+// granularity: a lane whose path ends (miss, light, absorption, Russian
+// roulette, max bounces) immediately starts its next sample, so every loop
+// iteration traces one ray per live lane instead of idling until the longest
+// path of the wave finishes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "crt_hip.h"
+#include "crt_device.h"
+
+using namespace crt;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_last_error;
+static int set_error(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+#define HIP_TRY(expr)                                                                           \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return set_error(CRT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// ------------------------------------------------------------------ kernels
+struct RenderParams {
+    const float4* __restrict__ nodes;
+    const float4* __restrict__ prims;
+    const float4* __restrict__ mats;
+    int n_nodes, n_mats;
+    int width, height, spp, max_bounces;
+    int accumulate;
+    uint32_t* __restrict__ rng;   // W*H*6 (v0..v4, d)
+    float* __restrict__ sum;      // W*H*3
+    unsigned long long* __restrict__ counters;  // crt_work_counters layout
+    crt_camera_desc cam;
+};
+
+struct TraceCounts { uint32_t boxes, tris, spheres; };
+
+// Closest hit over the threaded scene+mesh BVH.  Returns hit prim (SPHERE_BIT set for
+// spheres) or -1; `closest` = IntersectionTime of the accepted hit.
+// Semantics: BVHNode::hit (BVHNode.cuh:304-345), Mesh::hit (Mesh.cuh:55-110),
+// AABB::hit (AABB.cuh:123-146), rayTriangleIntersect (Mesh.cuh:266-308),
+// Sphere::hit (Sphere.cuh:27-47); closed-interval acceptance so ties go to the
+// later primitive, exactly as in the reference order.
+template <bool COUNT>
+__device__ __forceinline__ int trace(const float4* __restrict__ nodes, const float4* __restrict__ prims,
+                                     int n_nodes, V3 o, V3 d, float& closest, TraceCounts& cnt) {
+    const float INF = __builtin_inff();
+    // AABB::hit computes 1/d per node visit; the value is the same every time.
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    closest = INF;
+    int hit = -1;
+    int node = 0;
+    while (node < n_nodes) {
+        const float4 A = nodes[2 * node];
+        const float4 B = nodes[2 * node + 1];
+        const int a = __float_as_int(B.z);
+        const int b = __float_as_int(B.w);
+        const bool scene_level = (b == NODE_SCENE_INNER) || (b >= SPHERE_BIT);
+        const float tcl = scene_level ? INF : closest;
+        if (COUNT) cnt.boxes++;
+        const float t0x = (A.x - o.x) * inv.x, t0y = (A.y - o.y) * inv.y, t0z = (A.z - o.z) * inv.z;
+        const float t1x = (A.w - o.x) * inv.x, t1y = (B.x - o.y) * inv.y, t1z = (B.y - o.z) * inv.z;
+        float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+        float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+        tmin = fmaxf(tmin, 0.001f);
+        tmax = fminf(tmax, tcl);
+        const bool box_hit = !(tmax <= tmin);
+        int next = node + 1;
+        if (b < 0) {
+            if (!box_hit) next = a;
+        } else if (box_hit) {
+            if (b >= SPHERE_BIT) {
+                const int p = b - SPHERE_BIT;
+                if (COUNT) cnt.spheres++;
+                const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1];
+                const V3 oc = o - v3(f0.x, f0.y, f0.z);
+                const float qa = dot(d, d);
+                const float hb = dot(oc, d);
+                const float qc = dot(oc, oc) - f1.x;
+                const float disc = hb * hb - qa * qc;
+                if (!(disc < 0)) {
+                    const float sq = sqrtf(disc);
+                    float root = (-hb - sq) / qa;
+                    bool ok = true;
+                    if (root < 0.001f || root > closest) {
+                        root = (-hb + sq) / qa;
+                        if (root < 0.001f || root > closest) ok = false;
+                    }
+                    if (ok) { closest = root; hit = b; }
+                }
+            } else {
+                for (int k = 0; k < a; ++k) {
+                    const int p = b + k;
+                    if (COUNT) cnt.tris++;
+                    const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1], f2 = prims[3 * p + 2];
+                    const V3 e1 = v3(f0.w, f1.x, f1.y);
+                    const V3 e2 = v3(f1.z, f1.w, f2.x);
+                    const V3 h = cross(d, e2);
+                    const float det = dot(e1, h);
+                    if (fabsf(det) < 1e-8f) continue;
+                    const float f = 1.f / det;
+                    const V3 s = o - v3(f0.x, f0.y, f0.z);
+                    const float u = f * dot(s, h);
+                    if (u < 0.f || u > 1.f) continue;
+                    const V3 q = cross(s, e1);
+                    const float v = f * dot(d, q);
+                    if (v < 0.f || (u + v) > 1.f) continue;
+                    const float t = f * dot(e2, q);
+                    if (t < 0.001f || t > closest) continue;
+                    closest = t;
+                    hit = p;
+                }
+            }
+        }
+        node = next;
+    }
+    return hit;
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    return x;
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(256) void crt_render_kernel(RenderParams P) {
+    // 16x16 pixel tile per workgroup, 8x8 per wave64.
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool valid = x < P.width && y < P.height;
+    const int pix = valid ? y * P.width + x : 0;
+
+    Rng s{};
+    V3 pixel = v3(0.f, 0.f, 0.f);
+    int remaining = 0;
+    if (valid) {
+        const uint32_t* r = P.rng + 6 * (size_t)pix;
+        s.v0 = r[0]; s.v1 = r[1]; s.v2 = r[2]; s.v3 = r[3]; s.v4 = r[4]; s.d = r[5];
+        if (P.accumulate) pixel = v3(P.sum[3 * (size_t)pix], P.sum[3 * (size_t)pix + 1], P.sum[3 * (size_t)pix + 2]);
+        remaining = P.spp;
+    }
+    const crt_camera_desc& C = P.cam;
+    const V3 cpos = v3(C.origin[0], C.origin[1], C.origin[2]);
+    const V3 cllc = v3(C.lower_left[0], C.lower_left[1], C.lower_left[2]);
+    const V3 chor = v3(C.horizontal[0], C.horizontal[1], C.horizontal[2]);
+    const V3 cver = v3(C.vertical[0], C.vertical[1], C.vertical[2]);
+    const V3 cright = v3(C.right[0], C.right[1], C.right[2]);
+    const V3 cup = v3(C.up[0], C.up[1], C.up[2]);
+    const float fw = (float)P.width, fh = (float)P.height;
+
+    uint32_t rays = 0, paths = 0;
+    TraceCounts cnt{0, 0, 0};
+    V3 o = v3(0, 0, 0), d = v3(0, 0, 1), thr = v3(1, 1, 1);
+    int bounce = 0;
+    bool need_new = true;
+
+    for (;;) {
+        // ---- phase 1: make sure this lane has a ray to trace (or is done)
+        bool done = false;
+        for (;;) {
+            if (need_new) {
+                if (remaining == 0) { done = true; break; }
+                --remaining;
+                // Camera::getRay (Camera.cuh:32-44)
+                float da, db;
+                for (;;) {
+                    da = rand_pm1(s);
+                    db = rand_pm1(s);
+                    if (len2(v3(da, db, 0)) >= 1) continue;
+                    break;
+                }
+                const V3 rd = C.lens_radius * v3(da, db, 0);
+                const V3 off = v3(cright.x * rd.x, cright.y * rd.x, cright.z * rd.x) +
+                               v3(cup.x * rd.y, cup.y * rd.y, cup.z * rd.y);
+                const float u = ((float)x + uniform(s)) / fw;
+                const float v = ((float)y + uniform(s)) / fh;
+                o = cpos + off;
+                d = (((cllc + u * chor) + v * cver) - cpos) - off;
+                thr = v3(1.0f, 1.0f, 1.0f);
+                bounce = 0;
+                need_new = false;
+            }
+            // rayColor loop head (CUDAKernels.h:110-121)
+            if (bounce >= P.max_bounces) {            // fell out of the bounce loop: final_color = 0
+                pixel = pixel + v3(0.0f, 0.0f, 0.0f);
+                ++paths;
+                need_new = true;
+                continue;
+            }
+            if (bounce >= 3) {
+                float p = fmaxf(thr.x, fmaxf(thr.y, thr.z));
+                p = fminf(p, 0.95f);
+                if (uniform(s) > p) {
+                    pixel = pixel + v3(0.0f, 0.0f, 0.0f);
+                    ++paths;
+                    need_new = true;
+                    continue;
+                }
+                thr = (1 / p) * thr;
+            }
+            break;
+        }
+        if (done) break;
+
+        // ---- phase 2: closest hit (CUDAKernels.h:123)
+        ++rays;
+        float t;
+        const int hit = trace<COUNT>(P.nodes, P.prims, P.n_nodes, o, d, t, cnt);
+
+        // ---- phase 3: shade
+        if (hit < 0) {                                     // :137-142
+            pixel = pixel + thr * sky(d);
+            ++paths;
+            need_new = true;
+            continue;
+        }
+        const V3 hp = o + t * d;                           // Ray::pointAtDistance
+        V3 outward;
+        uint32_t mat;
+        if (hit >= SPHERE_BIT) {
+            const int p = hit - SPHERE_BIT;
+            const float4 f0 = P.prims[3 * p], f1 = P.prims[3 * p + 1];
+            outward = (1 / f0.w) * (hp - v3(f0.x, f0.y, f0.z));   // Sphere.cuh:44
+            mat = (uint32_t)__float_as_int(f1.y);
+        } else {
+            const float4 f0 = P.prims[3 * hit], f1 = P.prims[3 * hit + 1], f2 = P.prims[3 * hit + 2];
+            outward = unit(cross(v3(f0.w, f1.x, f1.y), v3(f1.z, f1.w, f2.x)));   // Mesh.cuh:303-304
+            mat = (uint32_t)__float_as_int(f2.y);
+        }
+        const bool front = dot(d, outward) < 0;            // HitInfo::setFaceNormal
+        const V3 n = front ? outward : -outward;
+        if (!(mat < (uint32_t)P.n_mats)) {                  // :127 invalid material: same ray again
+            ++bounce;
+            continue;
+        }
+        const float4 m0 = P.mats[3 * mat], m1 = P.mats[3 * mat + 1];
+        const int mtype = __float_as_int(m0.x);
+        if (mtype == CRT_LAMBERTIAN) {                      // Material.cuh:66-77
+            V3 sd = n + rand_unit_vector(s);
+            if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = n;
+            thr = thr * v3(m0.y, m0.z, m0.w);
+            o = hp;
+            d = sd;
+            ++bounce;
+        } else if (mtype == CRT_METAL) {                    // :89-96
+            V3 refl = reflect(d, n);
+            refl = unit(refl) + (m1.w * rand_unit_vector(s));
+            if (dot(refl, n) > 0) {
+                thr = thr * v3(m0.y, m0.z, m0.w);
+                o = hp;
+                d = refl;
+                ++bounce;
+            } else {                                        // absorbed: return Material::emit() = 0
+                pixel = pixel + v3(0.0f, 0.0f, 0.0f);
+                ++paths;
+                need_new = true;
+            }
+        } else if (mtype == CRT_DIELECTRIC) {               // :109-128
+            const float ior = P.mats[3 * mat + 2].x;
+            const float ri = front ? (1.0f / ior) : ior;
+            const V3 ud = unit(d);
+            const double cos_theta = fminf(dot(-ud, n), 1.0f);
+            const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+            const bool cannot_refract = (double)ri * sin_theta > 1.0;
+            V3 dir;
+            if (cannot_refract || schlick((float)cos_theta, ri) > uniform(s))
+                dir = reflect(ud, n);
+            else
+                dir = refract(ud, n, ri);
+            o = hp;
+            d = dir;
+            ++bounce;   // attenuation (1,1,1): thr unchanged (x*1 == x)
+        } else {                                            // DiffuseLight: return emit() raw
+            const V3 em = (mtype == CRT_DIFFUSE_LIGHT) ? v3(m1.x, m1.y, m1.z) : v3(0.0f, 0.0f, 0.0f);
+            pixel = pixel + em;
+            ++paths;
+            need_new = true;
+        }
+    }
+
+    if (valid) {
+        uint32_t* r = P.rng + 6 * (size_t)pix;
+        r[0] = s.v0; r[1] = s.v1; r[2] = s.v2; r[3] = s.v3; r[4] = s.v4; r[5] = s.d;
+        P.sum[3 * (size_t)pix] = pixel.x;
+        P.sum[3 * (size_t)pix + 1] = pixel.y;
+        P.sum[3 * (size_t)pix + 2] = pixel.z;
+    }
+    const uint64_t wr = wave_sum_u64(rays);
+    if (COUNT) {
+        const uint64_t wb = wave_sum_u64(cnt.boxes), wt = wave_sum_u64(cnt.tris);
+        const uint64_t ws = wave_sum_u64(cnt.spheres), wp = wave_sum_u64(paths);
+        if (lane == 0) {
+            atomicAdd(&P.counters[1], (unsigned long long)wb);
+            atomicAdd(&P.counters[2], (unsigned long long)wt);
+            atomicAdd(&P.counters[3], (unsigned long long)ws);
+            atomicAdd(&P.counters[4], (unsigned long long)wp);
+        }
+    }
+    if (lane == 0) atomicAdd(&P.counters[0], (unsigned long long)wr);
+}
+
+// curand_init(seed, subsequence_base + pixel, 0) (CUDAKernels.h:18-26): scrambled seed, then
+// v <- A^(2^67 * subsequence) v with seq[k] = A^(2^67 * 4^k) (one base-4 digit per matrix).
+__global__ __launch_bounds__(256) void crt_init_rand_kernel(uint32_t* __restrict__ rng, const uint32_t* __restrict__ seq,
+                                                            int n_pix, unsigned long long seed,
+                                                            unsigned long long subseq_base) {
+    const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= n_pix) return;
+    const uint32_t s0 = ((uint32_t)seed) ^ 0xaad26b49u;
+    const uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
+    const uint32_t t0 = 1099087573u * s0;
+    const uint32_t t1 = 2591861531u * s1;
+    uint32_t v[5] = {123456789u + t0, 362436069u ^ t0, 521288629u + t1, 88675123u ^ t1, 5783321u + t0};
+    const uint32_t dd = 6615241u + t1 + t0;
+    unsigned long long n = subseq_base + (unsigned long long)pix;
+    for (int k = 0; n; ++k, n >>= 2) {
+        const uint32_t reps = (uint32_t)(n & 3u);
+        const uint32_t* m = seq + 800 * k;
+        for (uint32_t q = 0; q < reps; ++q) {
+            uint32_t r[5] = {0, 0, 0, 0, 0};
+            for (int i = 0; i < 5; ++i) {
+                const uint32_t w = v[i];
+#pragma unroll 4
+                for (int j = 0; j < 32; ++j) {
+                    const uint32_t msk = 0u - ((w >> j) & 1u);
+                    const uint32_t* col = m + (i * 32 + j) * 5;
+#pragma unroll
+                    for (int c = 0; c < 5; ++c) r[c] ^= msk & col[c];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 5; ++c) v[c] = r[c];
+        }
+    }
+    uint32_t* o = rng + 6 * (size_t)pix;
+    o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3]; o[4] = v[4]; o[5] = dd;
+}
+
+// writeColor(data, idx, m_PixelSampleScale * pixel_color) (CUDAKernels.h:164, CRTUtility.cuh:21-32)
+__global__ __launch_bounds__(256) void crt_resolve_kernel(const float* __restrict__ sum, uint8_t* __restrict__ rgba,
+                                                          int n_pix, float scale) {
+    const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= n_pix) return;
+    const float r = scale * sum[3 * (size_t)pix];
+    const float g = scale * sum[3 * (size_t)pix + 1];
+    const float b = scale * sum[3 * (size_t)pix + 2];
+    uchar4 o;
+    o.x = to_u8(r); o.y = to_u8(g); o.z = to_u8(b); o.w = 255;
+    reinterpret_cast<uchar4*>(rgba)[pix] = o;
+}
+
+__global__ void crt_selftest_math_kernel(const float* a, const float* b, int n, float* out, double* out64) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = a[i], y = b[i];
+    out[4 * i] = x / y;
+    out[4 * i + 1] = sqrtf(fabsf(x));
+    out[4 * i + 2] = 1.0f / x;
+    const double dx = fabs((double)x * (double)y);
+    out[4 * i + 3] = (float)sqrt((double)fabsf(x));
+    out64[2 * i] = sqrt(dx);
+    out64[2 * i + 1] = 1.0 - dx * dx;
+}
+
+__global__ void crt_selftest_rng_kernel(const uint32_t* st_in, int n, int n_draw, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Rng s{st_in[6 * i], st_in[6 * i + 1], st_in[6 * i + 2], st_in[6 * i + 3], st_in[6 * i + 4], st_in[6 * i + 5]};
+    for (int k = 0; k < n_draw; ++k) out[(size_t)i * n_draw + k] = uniform(s);
+}
+
+// ------------------------------------------------------------------ host side
+namespace {
+
+// XORWOW single-step linear map and its 2^67*4^k powers (160 columns x 5 words).
+void xw_step(uint32_t v[5]) {
+    uint32_t t = v[0] ^ (v[0] >> 2);
+    v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+    v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+}
+void mv(const uint32_t* m, uint32_t v[5]) {
+    uint32_t r[5] = {0, 0, 0, 0, 0};
+    for (int i = 0; i < 160; ++i)
+        if (v[i / 32] & (1u << (i % 32)))
+            for (int k = 0; k < 5; ++k) r[k] ^= m[i * 5 + k];
+    std::memcpy(v, r, sizeof r);
+}
+void mm(const uint32_t* b, const uint32_t* a, uint32_t* c) {   // c = b o a
+    for (int col = 0; col < 160; ++col) {
+        uint32_t v[5];
+        std::memcpy(v, a + 5 * col, sizeof v);
+        mv(b, v);
+        std::memcpy(c + 5 * col, v, sizeof v);
+    }
+}
+const std::vector<uint32_t>& seq_tables() {
+    static std::vector<uint32_t> tab;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        tab.assign(32 * 800, 0);
+        std::vector<uint32_t> m(800), t(800);
+        for (int col = 0; col < 160; ++col) {
+            uint32_t v[5] = {0, 0, 0, 0, 0};
+            v[col / 32] = 1u << (col % 32);
+            xw_step(v);
+            std::memcpy(&m[5 * col], v, sizeof v);
+        }
+        for (int s = 0; s < 67; ++s) { mm(m.data(), m.data(), t.data()); m.swap(t); }
+        std::memcpy(&tab[0], m.data(), 800 * 4);
+        for (int k = 1; k < 32; ++k) {
+            mm(&tab[800 * (k - 1)], &tab[800 * (k - 1)], t.data());
+            mm(t.data(), t.data(), &tab[800 * k]);
+        }
+    });
+    return tab;
+}
+
+inline float i2f(int v) { float f; std::memcpy(&f, &v, 4); return f; }
+
+struct Flattener {
+    const crt_scene_desc* D;
+    std::vector<float4> nodes, prims;
+    std::vector<int> mesh_prim_base;
+    int max_depth = 0;
+    std::string err;
+
+    int push_node(const float bmin[3], const float bmax[3], int a, int b) {
+        nodes.push_back(make_float4(bmin[0], bmin[1], bmin[2], bmax[0]));
+        nodes.push_back(make_float4(bmax[1], bmax[2], i2f(a), i2f(b)));
+        return (int)(nodes.size() / 2) - 1;
+    }
+    void set_a(int idx, int a) { nodes[2 * idx + 1].z = i2f(a); }
+    int count() const { return (int)(nodes.size() / 2); }
+
+    bool emit_mesh(int m, int ni, int depth) {
+        const crt_mesh_desc& M = D->meshes[m];
+        if (ni < 0 || ni >= M.node_count) { err = "mesh node index out of range"; return false; }
+        if (depth > 4096) { err = "mesh BVH too deep"; return false; }
+        max_depth = std::max(max_depth, depth);
+        const crt_bvh_node_desc& N = M.nodes[ni];
+        if (!N.is_leaf) {
+            int idx = push_node(N.bmin, N.bmax, 0, NODE_MESH_INNER);
+            if (!emit_mesh(m, N.left, depth + 1) || !emit_mesh(m, N.right, depth + 1)) return false;
+            set_a(idx, count());
+        } else {
+            if (N.obj_index < 0 || N.obj_count < 0 || N.obj_index % 3 || N.obj_count % 3 ||
+                (uint64_t)N.obj_index + N.obj_count > M.index_count) { err = "bad mesh leaf range"; return false; }
+            long first = mesh_prim_base[m] + N.obj_index / 3;
+            if (first >= SPHERE_BIT) { err = "too many primitives"; return false; }
+            push_node(N.bmin, N.bmax, N.obj_count / 3, (int)first);
+        }
+        return true;
+    }
+    bool emit_scene(int ni, int depth) {
+        if (ni < 0 || ni >= D->n_scene_nodes) { err = "scene node index out of range"; return false; }
+        if (depth > 4096) { err = "scene BVH too deep"; return false; }
+        max_depth = std::max(max_depth, depth);
+        const crt_bvh_node_desc& N = D->scene_nodes[ni];
+        if (!N.is_leaf) {
+            int idx = push_node(N.bmin, N.bmax, 0, NODE_SCENE_INNER);
+            if (!emit_scene(N.left, depth + 1) || !emit_scene(N.right, depth + 1)) return false;
+            set_a(idx, count());
+            return true;
+        }
+        if (N.obj_index < 0 || N.obj_index >= D->n_objects) { err = "scene leaf object out of range"; return false; }
+        const crt_object_desc& O = D->objects[N.obj_index];
+        if (O.kind == CRT_OBJECT_MESH) {
+            if (O.index < 0 || O.index >= D->n_meshes) { err = "mesh object index out of range"; return false; }
+            int idx = push_node(N.bmin, N.bmax, 0, NODE_SCENE_INNER);
+            if (D->meshes[O.index].node_count > 0 && !emit_mesh(O.index, 0, depth + 1)) return false;
+            set_a(idx, count());
+        } else if (O.kind == CRT_OBJECT_SPHERE) {
+            if (O.index < 0 || O.index >= D->n_spheres) { err = "sphere object index out of range"; return false; }
+            const crt_sphere_desc& S = D->spheres[O.index];
+            int p = (int)(prims.size() / 3);
+            if (p >= SPHERE_BIT) { err = "too many primitives"; return false; }
+            prims.push_back(make_float4(S.center[0], S.center[1], S.center[2], S.radius));
+            prims.push_back(make_float4(S.radius * S.radius, i2f(S.material), 0.f, 0.f));   // Sphere.cuh:21
+            prims.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+            push_node(N.bmin, N.bmax, 0, SPHERE_BIT | p);
+        } else {
+            err = "unknown object kind";
+            return false;
+        }
+        return true;
+    }
+    bool build_triangles() {
+        mesh_prim_base.assign(D->n_meshes, 0);
+        for (int m = 0; m < D->n_meshes; ++m) {
+            const crt_mesh_desc& M = D->meshes[m];
+            if ((uint64_t)M.index_offset + M.index_count > D->n_indices ||
+                (uint64_t)M.vertex_offset + M.vertex_count > D->n_positions ||
+                (uint64_t)M.face_offset + M.index_count / 3 > D->n_faces || M.index_count % 3) {
+                err = "mesh ranges exceed the scene arrays";
+                return false;
+            }
+            mesh_prim_base[m] = (int)(prims.size() / 3);
+            for (uint32_t t = 0; t < M.index_count / 3; ++t) {
+                uint32_t iv[3];
+                for (int c = 0; c < 3; ++c) {
+                    iv[c] = D->indices[M.index_offset + 3 * t + c];
+                    if (iv[c] >= M.vertex_count) { err = "vertex index out of range"; return false; }
+                }
+                const float* p0 = D->positions + 3 * ((size_t)M.vertex_offset + iv[0]);
+                const float* p1 = D->positions + 3 * ((size_t)M.vertex_offset + iv[1]);
+                const float* p2 = D->positions + 3 * ((size_t)M.vertex_offset + iv[2]);
+                const float e1[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};   // Mesh.cuh:277
+                const float e2[3] = {p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2]};   // Mesh.cuh:278
+                const uint32_t mat = (uint32_t)(D->face_materials[M.face_offset + t] + (int32_t)M.material_id_offset);
+                prims.push_back(make_float4(p0[0], p0[1], p0[2], e1[0]));
+                prims.push_back(make_float4(e1[1], e1[2], e2[0], e2[1]));
+                prims.push_back(make_float4(e2[2], i2f((int)mat), 0.f, 0.f));
+            }
+        }
+        return true;
+    }
+};
+
+}  // namespace
+
+struct crt_scene {
+    int device = 0;
+    float4* d_nodes = nullptr;
+    float4* d_prims = nullptr;
+    float4* d_mats = nullptr;
+    int n_nodes = 0, n_prims = 0, n_mats = 0;
+    int max_depth = 0;
+};
+
+struct crt_renderer {
+    int device = 0, width = 0, height = 0;
+    uint32_t* d_rng = nullptr;
+    float* d_sum = nullptr;
+    uint8_t* d_rgba = nullptr;
+    uint32_t* d_seq = nullptr;
+    unsigned long long* d_counters = nullptr;
+    crt_camera_desc cam{};
+    bool has_camera = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+};
+
+namespace {
+int use_device(int dev) {
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (n <= 0) return set_error(CRT_ERR_NO_DEVICE, "no HIP device visible");
+    if (dev < 0 || dev >= n) return set_error(CRT_ERR_INVALID_ARGUMENT, "device ordinal out of range");
+    HIP_TRY(hipSetDevice(dev));
+    return CRT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int crt_abi_version(void) { return CRT_ABI_VERSION; }
+const char* crt_last_error(void) { return g_last_error.c_str(); }
+
+int crt_device_count(int* out) {
+    if (!out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null out");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    *out = (e == hipSuccess) ? n : 0;
+    return CRT_OK;
+}
+
+int crt_scene_create(const crt_scene_desc* D, int device, crt_scene** out) {
+    if (!D || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    if (D->n_scene_nodes <= 0 || !D->scene_nodes) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene has no BVH nodes");
+    if (D->n_materials < 0 || (D->n_materials > 0 && !D->materials)) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad materials");
+    Flattener F{D};
+    if (!F.build_triangles() || !F.emit_scene(0, 0)) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene: " + F.err);
+    std::vector<float4> mats;
+    for (int i = 0; i < D->n_materials; ++i) {
+        const crt_material_desc& M = D->materials[i];
+        mats.push_back(make_float4(i2f(M.type), M.albedo[0], M.albedo[1], M.albedo[2]));
+        mats.push_back(make_float4(M.emission[0], M.emission[1], M.emission[2], M.roughness < 1.f ? M.roughness : 1.f));
+        mats.push_back(make_float4(M.ior, 0.f, 0.f, 0.f));
+    }
+    if (int rc = use_device(device)) return rc;
+    crt_scene* S = new (std::nothrow) crt_scene;
+    if (!S) return set_error(CRT_ERR_OUT_OF_MEMORY, "host allocation failed");
+    S->device = device;
+    S->n_nodes = F.count();
+    S->n_prims = (int)(F.prims.size() / 3);
+    S->n_mats = D->n_materials;
+    S->max_depth = F.max_depth;
+    auto up = [&](float4** dst, const std::vector<float4>& src) -> hipError_t {
+        size_t bytes = std::max<size_t>(src.size(), 1) * sizeof(float4);
+        hipError_t e = hipMalloc((void**)dst, bytes);
+        if (e != hipSuccess) return e;
+        if (!src.empty()) e = hipMemcpy(*dst, src.data(), src.size() * sizeof(float4), hipMemcpyHostToDevice);
+        return e;
+    };
+    hipError_t e;
+    if ((e = up(&S->d_nodes, F.nodes)) != hipSuccess || (e = up(&S->d_prims, F.prims)) != hipSuccess ||
+        (e = up(&S->d_mats, mats)) != hipSuccess) {
+        crt_scene_destroy(S);
+        return set_error(CRT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e));
+    }
+    *out = S;
+    return CRT_OK;
+}
+
+int crt_scene_get_stats(const crt_scene* S, crt_scene_stats* out) {
+    if (!S || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    out->device_nodes = S->n_nodes;
+    out->device_prims = S->n_prims;
+    out->device_bytes = (int64_t)S->n_nodes * 32 + (int64_t)S->n_prims * 48 + (int64_t)S->n_mats * 48;
+    out->max_depth = S->max_depth;
+    out->n_materials = S->n_mats;
+    return CRT_OK;
+}
+
+void crt_scene_destroy(crt_scene* S) {
+    if (!S) return;
+    (void)hipSetDevice(S->device);
+    if (S->d_nodes) (void)hipFree(S->d_nodes);
+    if (S->d_prims) (void)hipFree(S->d_prims);
+    if (S->d_mats) (void)hipFree(S->d_mats);
+    delete S;
+}
+
+int crt_renderer_create(int width, int height, int device, crt_renderer** out) {
+    if (!out || width <= 0 || height <= 0 || (long long)width * height > (1LL << 31) / 6)
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "bad renderer size");
+    *out = nullptr;
+    if (int rc = use_device(device)) return rc;
+    crt_renderer* R = new (std::nothrow) crt_renderer;
+    if (!R) return set_error(CRT_ERR_OUT_OF_MEMORY, "host allocation failed");
+    R->device = device; R->width = width; R->height = height;
+    const size_t n = (size_t)width * height;
+    const auto& tab = seq_tables();
+    hipError_t e;
+    if ((e = hipMalloc((void**)&R->d_rng, n * 6 * 4)) != hipSuccess ||
+        (e = hipMalloc((void**)&R->d_sum, n * 3 * 4)) != hipSuccess ||
+        (e = hipMalloc((void**)&R->d_rgba, n * 4)) != hipSuccess ||
+        (e = hipMalloc((void**)&R->d_seq, tab.size() * 4)) != hipSuccess ||
+        (e = hipMalloc((void**)&R->d_counters, 8 * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMemcpy(R->d_seq, tab.data(), tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemset(R->d_sum, 0, n * 3 * 4)) != hipSuccess ||
+        (e = hipMemset(R->d_rgba, 0, n * 4)) != hipSuccess ||
+        (e = hipMemset(R->d_counters, 0, 8 * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipEventCreate(&R->ev0)) != hipSuccess || (e = hipEventCreate(&R->ev1)) != hipSuccess) {
+        crt_renderer_destroy(R);
+        return set_error(e == hipErrorOutOfMemory ? CRT_ERR_OUT_OF_MEMORY : CRT_ERR_HIP,
+                         std::string("renderer allocation: ") + hipGetErrorString(e));
+    }
+    *out = R;
+    return CRT_OK;
+}
+
+void crt_renderer_destroy(crt_renderer* R) {
+    if (!R) return;
+    (void)hipSetDevice(R->device);
+    if (R->d_rng) (void)hipFree(R->d_rng);
+    if (R->d_sum) (void)hipFree(R->d_sum);
+    if (R->d_rgba) (void)hipFree(R->d_rgba);
+    if (R->d_seq) (void)hipFree(R->d_seq);
+    if (R->d_counters) (void)hipFree(R->d_counters);
+    if (R->ev0) (void)hipEventDestroy(R->ev0);
+    if (R->ev1) (void)hipEventDestroy(R->ev1);
+    delete R;
+}
+
+int crt_renderer_init_rand(crt_renderer* R, unsigned long long seed, unsigned long long subseq_base, void* stream) {
+    if (!R) return set_error(CRT_ERR_INVALID_ARGUMENT, "null renderer");
+    HIP_TRY(hipSetDevice(R->device));
+    const int n = R->width * R->height;
+    hipLaunchKernelGGL(crt_init_rand_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, R->d_rng,
+                       R->d_seq, n, seed, subseq_base);
+    HIP_TRY(hipGetLastError());
+    return CRT_OK;
+}
+
+int crt_renderer_set_camera(crt_renderer* R, const crt_camera_desc* cam) {
+    if (!R || !cam) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    R->cam = *cam;
+    R->has_camera = true;
+    return CRT_OK;
+}
+
+int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bounces, unsigned flags, void* stream) {
+    if (!R || !S) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    if (!R->has_camera) return set_error(CRT_ERR_INVALID_ARGUMENT, "camera not set");
+    if (spp < 0 || max_bounces < 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "negative spp / bounces");
+    if (S->device != R->device) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene and renderer on different devices");
+    HIP_TRY(hipSetDevice(R->device));
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(R->d_counters, 0, 8 * sizeof(unsigned long long), st));
+    RenderParams P;
+    P.nodes = S->d_nodes; P.prims = S->d_prims; P.mats = S->d_mats;
+    P.n_nodes = S->n_nodes; P.n_mats = S->n_mats;
+    P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
+    P.accumulate = (flags & CRT_RENDER_ACCUMULATE) ? 1 : 0;
+    P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
+    dim3 grid((R->width + 15) / 16, (R->height + 15) / 16), block(256);
+    HIP_TRY(hipEventRecord(R->ev0, st));
+    if (flags & CRT_RENDER_COUNT_WORK)
+        hipLaunchKernelGGL(crt_render_kernel<true>, grid, block, 0, st, P);
+    else
+        hipLaunchKernelGGL(crt_render_kernel<false>, grid, block, 0, st, P);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(R->ev1, st));
+    R->timed = true;
+    return CRT_OK;
+}
+
+int crt_renderer_resolve(crt_renderer* R, float scale, void* stream) {
+    if (!R) return set_error(CRT_ERR_INVALID_ARGUMENT, "null renderer");
+    HIP_TRY(hipSetDevice(R->device));
+    const int n = R->width * R->height;
+    hipLaunchKernelGGL(crt_resolve_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, R->d_sum,
+                       R->d_rgba, n, scale);
+    HIP_TRY(hipGetLastError());
+    return CRT_OK;
+}
+
+int crt_renderer_render_frame(crt_renderer* R, const crt_scene* S, void* stream) {
+    if (!R) return set_error(CRT_ERR_INVALID_ARGUMENT, "null renderer");
+    if (!R->has_camera) return set_error(CRT_ERR_INVALID_ARGUMENT, "camera not set");
+    if (int rc = crt_renderer_render(R, S, R->cam.samples_per_pixel, 20, 0u, stream)) return rc;
+    if (int rc = crt_renderer_resolve(R, R->cam.pixel_sample_scale, stream)) return rc;
+    return crt_renderer_synchronize(R, stream);
+}
+
+int crt_renderer_synchronize(crt_renderer* R, void* stream) {
+    if (!R) return set_error(CRT_ERR_INVALID_ARGUMENT, "null renderer");
+    HIP_TRY(hipSetDevice(R->device));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return CRT_OK;
+}
+
+static int read_dev(crt_renderer* R, void* dst, const void* src, size_t bytes) {
+    if (!R || !dst) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(hipSetDevice(R->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return CRT_OK;
+}
+int crt_renderer_read_linear(crt_renderer* R, float* out) {
+    return R ? read_dev(R, out, R->d_sum, (size_t)R->width * R->height * 12) : set_error(CRT_ERR_INVALID_ARGUMENT, "null");
+}
+int crt_renderer_read_rgba8(crt_renderer* R, uint8_t* out) {
+    return R ? read_dev(R, out, R->d_rgba, (size_t)R->width * R->height * 4) : set_error(CRT_ERR_INVALID_ARGUMENT, "null");
+}
+int crt_renderer_read_rng(crt_renderer* R, uint32_t* out) {
+    return R ? read_dev(R, out, R->d_rng, (size_t)R->width * R->height * 24) : set_error(CRT_ERR_INVALID_ARGUMENT, "null");
+}
+int crt_renderer_write_linear(crt_renderer* R, const float* in) {
+    if (!R || !in) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(hipSetDevice(R->device));
+    HIP_TRY(hipMemcpy(R->d_sum, in, (size_t)R->width * R->height * 12, hipMemcpyHostToDevice));
+    return CRT_OK;
+}
+int crt_renderer_get_counters(crt_renderer* R, crt_work_counters* out) {
+    if (!R || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    unsigned long long c[8];
+    if (int rc = read_dev(R, c, R->d_counters, sizeof c)) return rc;
+    out->rays = c[0]; out->box_tests = c[1]; out->tri_tests = c[2]; out->sphere_tests = c[3]; out->paths = c[4];
+    return CRT_OK;
+}
+float* crt_renderer_linear_device_ptr(crt_renderer* R) { return R ? R->d_sum : nullptr; }
+uint8_t* crt_renderer_rgba_device_ptr(crt_renderer* R) { return R ? R->d_rgba : nullptr; }
+uint32_t* crt_renderer_rng_device_ptr(crt_renderer* R) { return R ? R->d_rng : nullptr; }
+
+float crt_renderer_last_kernel_ms(crt_renderer* R) {
+    if (!R || !R->timed) return -1.f;
+    if (hipSetDevice(R->device) != hipSuccess || hipEventSynchronize(R->ev1) != hipSuccess) return -1.f;
+    float ms = -1.f;
+    if (hipEventElapsedTime(&ms, R->ev0, R->ev1) != hipSuccess) return -1.f;
+    return ms;
+}
+
+int crt_selftest_math(const float* a, const float* b, int n, float* out, double* out64) {
+    if (!a || !b || !out || !out64 || n <= 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    if (int rc = use_device(0)) return rc;
+    float *da, *db, *dout;
+    double* d64;
+    HIP_TRY(hipMalloc((void**)&da, n * 4));
+    HIP_TRY(hipMalloc((void**)&db, n * 4));
+    HIP_TRY(hipMalloc((void**)&dout, n * 16));
+    HIP_TRY(hipMalloc((void**)&d64, n * 16));
+    HIP_TRY(hipMemcpy(da, a, n * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(db, b, n * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(crt_selftest_math_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, da, db, n, dout, d64);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(out, dout, n * 16, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(out64, d64, n * 16, hipMemcpyDeviceToHost));
+    (void)hipFree(da); (void)hipFree(db); (void)hipFree(dout); (void)hipFree(d64);
+    return CRT_OK;
+}
+
+int crt_selftest_rng(unsigned long long seed, const unsigned long long* subseq, int n, int n_draw,
+                     uint32_t* state_out, float* uniforms_out) {
+    if (!subseq || !state_out || !uniforms_out || n <= 0 || n_draw < 0)
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    if (int rc = use_device(0)) return rc;
+    const auto& tab = seq_tables();
+    uint32_t *dseq, *dst;
+    float* du;
+    HIP_TRY(hipMalloc((void**)&dseq, tab.size() * 4));
+    HIP_TRY(hipMalloc((void**)&dst, (size_t)n * 24));
+    HIP_TRY(hipMalloc((void**)&du, (size_t)n * std::max(n_draw, 1) * 4));
+    HIP_TRY(hipMemcpy(dseq, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+    for (int i = 0; i < n; ++i) {   // one launch per subsequence keeps the kernel identical to the renderer's
+        hipLaunchKernelGGL(crt_init_rand_kernel, dim3(1), dim3(64), 0, 0, dst + 6 * i, dseq, 1, seed, subseq[i]);
+    }
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(crt_selftest_rng_kernel, dim3((n + 63) / 64), dim3(64), 0, 0, dst, n, n_draw, du);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(state_out, dst, (size_t)n * 24, hipMemcpyDeviceToHost));
+    if (n_draw) HIP_TRY(hipMemcpy(uniforms_out, du, (size_t)n * n_draw * 4, hipMemcpyDeviceToHost));
+    (void)hipFree(dseq); (void)hipFree(dst); (void)hipFree(du);
+    return CRT_OK;
+}
+
+}  // extern "C"

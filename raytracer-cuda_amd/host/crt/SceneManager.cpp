@@ -1,0 +1,217 @@
+// SceneManager.cpp — see SceneManager.h.  Line references: CudaRayTracer/src/SceneManager.h
+// unless noted.
+#include "SceneManager.h"
+
+#include <cmath>
+#include <limits>
+#include <set>
+#include <stdexcept>
+
+#include "ObjLoader.h"
+
+SceneManager::SceneManager(int width, int height, int device) : m_Width(width), m_Height(height), m_Device(device) {}
+
+SceneManager::~SceneManager() {
+    if (m_Scene) crt_scene_destroy(m_Scene);
+}
+
+void SceneManager::initializeScene(const CUDAHelpers::RenderConfig& renderConfig, void* randState) {
+    (void)renderConfig;
+    (void)randState;
+    buildHostScene();
+    uploadScene();
+}
+
+void SceneManager::buildHostScene() {
+    m_MeshData.clear();
+    m_SceneMaterialsData.clear();
+    initMeshes();
+    createWorld();
+}
+
+void SceneManager::uploadScene() {
+    if (m_Scene) {
+        crt_scene_destroy(m_Scene);
+        m_Scene = nullptr;
+    }
+    crt_scene_desc d = sceneDesc();
+    CRT_CHECK(crt_scene_create(&d, m_Device, &m_Scene));
+}
+
+// :100-196
+void SceneManager::initMeshes() {
+    std::vector<MeshData> allMeshData;
+    for (const auto& file : m_ModelFiles) loadObject(file, allMeshData);
+    m_MeshData = allMeshData;
+    const int n = (int)allMeshData.size();
+    m_VertexOffsets.assign(n, 0); m_IndexOffsets.assign(n, 0); m_VertexCounts.assign(n, 0);
+    m_IndexCounts.assign(n, 0); m_FaceMatOffsets.assign(n, 0); m_FaceCounts.assign(n, 0);
+    std::vector<uint32_t> uniquePerMesh;
+    m_Positions.clear(); m_Indices.clear(); m_FaceMats.clear();
+    for (int i = 0; i < n; i++) {
+        const MeshData& md = allMeshData[i];
+        m_VertexOffsets[i] = (uint32_t)(m_Positions.size() / 3);
+        m_IndexOffsets[i] = (uint32_t)m_Indices.size();
+        m_FaceMatOffsets[i] = (uint32_t)m_FaceMats.size();
+        for (const Vertex& v : md.vertices)
+            for (int c = 0; c < 3; ++c) m_Positions.push_back(v.Position[c]);
+        m_Indices.insert(m_Indices.end(), md.indices.begin(), md.indices.end());
+        m_FaceMats.insert(m_FaceMats.end(), md.faceMaterialIds.begin(), md.faceMaterialIds.end());
+        std::set<int> uniq(md.faceMaterialIds.begin(), md.faceMaterialIds.end());   // :143-145
+        uniquePerMesh.push_back((uint32_t)uniq.size());
+        m_VertexCounts[i] = (uint32_t)md.vertices.size();
+        m_IndexCounts[i] = (uint32_t)md.indices.size();
+        m_FaceCounts[i] = (uint32_t)md.faceMaterialIds.size();
+    }
+    m_MaterialIDOffsets.assign(n, 0);
+    m_Meshes.assign(n, crt_mesh_desc{});
+    m_MeshBVH.assign(n, {});
+    m_MeshBoxes.assign(n, CRT::AABB());
+    for (int i = 0; i < n; i++) {
+        m_MaterialIDOffsets[i] = i == 0 ? 0 : uniquePerMesh[i - 1];                     // :177 (previous mesh only)
+        for (uint32_t k = 0; k < m_IndexCounts[i]; ++k)
+            if (m_Indices[m_IndexOffsets[i] + k] >= m_VertexCounts[i])
+                throw std::runtime_error("mesh index out of range of its vertex slots");
+        // Mesh ctor + buildBVHMesh (CUDAKernels.h:92-100, Mesh.cuh:18-53)
+        CRT::BuildStatus st = CRT::buildMeshBVH(m_Positions.data() + 3 * (size_t)m_VertexOffsets[i], m_VertexCounts[i],
+                                                m_Indices.data() + m_IndexOffsets[i], m_FaceMats.data() + m_FaceMatOffsets[i],
+                                                m_IndexCounts[i], &m_MeshBoxes[i], &m_MeshBVH[i]);
+        if (!st.ok) throw std::runtime_error(st.error);
+    }
+    for (int i = 0; i < n; i++) {
+        crt_mesh_desc& d = m_Meshes[i];
+        d.vertex_offset = m_VertexOffsets[i];
+        d.vertex_count = m_VertexCounts[i];
+        d.index_offset = m_IndexOffsets[i];
+        d.index_count = m_IndexCounts[i];
+        d.face_offset = m_FaceMatOffsets[i];
+        d.material_id_offset = m_MaterialIDOffsets[i];
+        d.nodes = m_MeshBVH[i].data();
+        d.node_count = (int32_t)m_MeshBVH[i].size();
+        const CRT::AABB& b = m_MeshBoxes[i];
+        d.aabb[0] = b.x.min; d.aabb[1] = b.y.min; d.aabb[2] = b.z.min;
+        d.aabb[3] = b.x.max; d.aabb[4] = b.y.max; d.aabb[5] = b.z.max;
+    }
+}
+
+// :198-329
+void SceneManager::loadObject(const std::string& filename, std::vector<MeshData>& meshDataList) {
+    size_t last = filename.find_last_of("/\\");
+    std::string base_dir = last != std::string::npos ? filename.substr(0, last + 1) : "./";
+    CRT::ObjData od;
+    std::string err;
+    if (!CRT::LoadObj(&od, &err, filename.c_str(), base_dir.c_str())) {
+        if (!err.empty()) std::cerr << "ObjLoader error:   " << err << std::endl;
+        throw std::runtime_error("Failed to load object: " + filename);
+    }
+    for (const auto& mat : od.materials) {                                           // :222-247
+        CRT::MaterialType mt = CRT::MaterialType::Lambertian;
+        if (mat.emission[0] > 0.f || mat.emission[1] > 0.f || mat.emission[2] > 0.f) mt = CRT::MaterialType::DiffuseLight;
+        else if (mat.dissolve < 1.f) mt = CRT::MaterialType::Dielectric;
+        else if (mat.specular[0] > 0.f) mt = CRT::MaterialType::Metal;
+        float r = 0.f;
+        if (mt == CRT::MaterialType::Metal) {
+            if (mat.roughness > 0.f) r = mat.roughness;
+            else r = sqrtf(2.f / (mat.shininess + 2.f));
+        }
+        float ior = (mt == CRT::MaterialType::Dielectric ? mat.ior : 1.f);
+        m_SceneMaterialsData.emplace_back(mt, CRT::Vec3(mat.diffuse[0], mat.diffuse[1], mat.diffuse[2]), r, ior,
+                                          CRT::Vec3(mat.emission[0], mat.emission[1], mat.emission[2]));
+    }
+    MeshData meshData;
+    const size_t nTri = od.triMaterial.size();
+    if (nTri > 0) meshData.vertices.resize(od.vertices.size());                         // :253 (3x too many slots)
+    for (size_t f = 0; f < nTri; ++f) {
+        int faceMatId = od.triMaterial[f];                                            // :259-265
+        if (faceMatId < 0 || faceMatId >= static_cast<int>(m_SceneMaterialsData.size())) faceMatId = 0;
+        meshData.faceMaterialIds.push_back(faceMatId);
+        for (int v = 0; v < 3; v++) {
+            const int32_t vi = od.triIndices[3 * f + v];
+            if (vi < 0 || 3 * (size_t)vi + 2 >= od.vertices.size())
+                throw std::runtime_error("face vertex index out of range in " + filename);
+            Vertex vertex{};
+            vertex.Position = CRT::Vec3(od.vertices[3 * vi], od.vertices[3 * vi + 1], od.vertices[3 * vi + 2]);
+            meshData.indices.push_back((uint32_t)vi);
+            meshData.vertices[vi] = vertex;                                           // :300 last write wins
+        }
+    }
+    meshDataList.push_back(meshData);
+    // :307-325 — normalise every mesh loaded so far
+    CRT::Vec3 minBounds(std::numeric_limits<float>::max());
+    CRT::Vec3 maxBounds(std::numeric_limits<float>::lowest());
+    for (auto& md : meshDataList)
+        for (const auto& vertex : md.vertices) {
+            minBounds = CRT::Vec3::min(minBounds, vertex.Position);
+            maxBounds = CRT::Vec3::max(maxBounds, vertex.Position);
+        }
+    CRT::Vec3 center = (minBounds + maxBounds) * 0.5f;
+    float scale = 0.6f / (maxBounds - minBounds).maxComponent();
+    for (auto& md : meshDataList)
+        for (auto& vertex : md.vertices) vertex.Position = (vertex.Position - center) * scale;
+}
+
+// createRandomWorld (CUDAKernels.h:28-84) + createBVH (:86-90)
+void SceneManager::createWorld() {
+    const int MAX_OBJECTS = 500, MAX_MATERIALS = 500;   // HittableList.cuh:328-329
+    m_Materials.clear(); m_Spheres.clear(); m_Objects.clear();
+    auto addMaterial = [&](const crt_material_desc& m) -> int {
+        if ((int)m_Materials.size() < MAX_MATERIALS) { m_Materials.push_back(m); return (int)m_Materials.size() - 1; }
+        return -1;
+    };
+    for (const auto& md : m_SceneMaterialsData) {
+        crt_material_desc m{};
+        m.type = (int32_t)md.getType();
+        CRT::Vec3 a = md.getAlbedo(), e = md.getEmission();
+        for (int c = 0; c < 3; ++c) { m.albedo[c] = a[c]; m.emission[c] = e[c]; }
+        m.roughness = md.getRoughness() < 1.f ? md.getRoughness() : 1.f;          // Metal ctor, Material.cuh:86
+        m.ior = md.getIOR();
+        addMaterial(m);
+    }
+    std::vector<CRT::AABB> boxes;
+    auto addObject = [&](int kind, int index, const CRT::AABB& box) {
+        if ((int)m_Objects.size() < MAX_OBJECTS) { m_Objects.push_back({kind, index}); boxes.push_back(box); }
+    };
+    for (int i = 0; i < (int)m_Meshes.size(); ++i) addObject(CRT_OBJECT_MESH, i, m_MeshBoxes[i]);
+    auto addSphere = [&](CRT::Vec3 c, float r, int mat) {
+        crt_sphere_desc s{{c[0], c[1], c[2]}, r, mat};
+        m_Spheres.push_back(s);
+        CRT::Vec3 rv(r, r, r);
+        addObject(CRT_OBJECT_SPHERE, (int)m_Spheres.size() - 1, CRT::AABB(c - rv, c + rv));   // Sphere.cuh:20-25
+    };
+    crt_material_desc ground{};
+    ground.type = CRT_LAMBERTIAN;
+    ground.albedo[0] = ground.albedo[1] = ground.albedo[2] = 0.5f;
+    ground.ior = 1.f;
+    int gi = addMaterial(ground);
+    addSphere(CRT::Vec3(0, -1000, 0), 999, gi);
+    crt_material_desc metal{};
+    metal.type = CRT_METAL;
+    metal.albedo[0] = (float)0.7; metal.albedo[1] = (float)0.6; metal.albedo[2] = (float)0.5;
+    metal.roughness = 0.0f;
+    metal.ior = 1.f;
+    int mi = addMaterial(metal);
+    addSphere(CRT::Vec3((float)0.2, (float)0.2, 0), 0.05f, mi);
+    CRT::BuildStatus st = CRT::buildSceneBVH(boxes, &m_SceneBVH);
+    if (!st.ok) throw std::runtime_error(st.error);
+}
+
+crt_scene_desc SceneManager::sceneDesc() const {
+    crt_scene_desc d{};
+    d.positions = m_Positions.data();
+    d.n_positions = m_Positions.size() / 3;
+    d.indices = m_Indices.data();
+    d.n_indices = m_Indices.size();
+    d.face_materials = m_FaceMats.data();
+    d.n_faces = m_FaceMats.size();
+    d.meshes = m_Meshes.data();
+    d.n_meshes = (int32_t)m_Meshes.size();
+    d.spheres = m_Spheres.data();
+    d.n_spheres = (int32_t)m_Spheres.size();
+    d.objects = m_Objects.data();
+    d.n_objects = (int32_t)m_Objects.size();
+    d.scene_nodes = m_SceneBVH.data();
+    d.n_scene_nodes = (int32_t)m_SceneBVH.size();
+    d.materials = m_Materials.data();
+    d.n_materials = (int32_t)m_Materials.size();
+    return d;
+}

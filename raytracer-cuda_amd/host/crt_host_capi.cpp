@@ -1,0 +1,109 @@
+// crt_host_capi.cpp — C ABI over the host C++ scene pipeline (include/crt_host.h).
+#include <cstring>
+#include <exception>
+#include <string>
+
+#include "crt/Camera.h"
+#include "crt/SceneManager.h"
+#include "crt_host.h"
+
+struct crth_scene {
+    SceneManager sm{1, 1};
+    // unpermuted loader output (before the mesh BVH builds reorder indices / face materials)
+    std::vector<uint32_t> idx0;
+    std::vector<int32_t> fmat0;
+};
+
+static thread_local std::string g_err;
+
+extern "C" {
+
+const char* crth_last_error(void) { return g_err.c_str(); }
+
+int crth_scene_load(const char* const* files, int n, crth_scene** out) {
+    if (!files || n < 0 || !out) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    *out = nullptr;
+    try {
+        crth_scene* s = new crth_scene;
+        std::vector<std::string> v;
+        for (int i = 0; i < n; ++i) v.emplace_back(files[i]);
+        s->sm.setModelFiles(v);
+        s->sm.buildHostScene();
+        // rebuild the unpermuted arrays from MeshData (the loader output)
+        for (const auto& md : s->sm.meshData()) {
+            s->idx0.insert(s->idx0.end(), md.indices.begin(), md.indices.end());
+            s->fmat0.insert(s->fmat0.end(), md.faceMaterialIds.begin(), md.faceMaterialIds.end());
+        }
+        *out = s;
+        return CRT_OK;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return CRT_ERR_INVALID_ARGUMENT;
+    }
+}
+
+void crth_scene_destroy(crth_scene* s) { delete s; }
+
+int crth_scene_desc(const crth_scene* s, crt_scene_desc* out) {
+    if (!s || !out) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    *out = s->sm.sceneDesc();
+    return CRT_OK;
+}
+
+int crth_scene_upload(const crth_scene* s, int device, crt_scene** out) {
+    if (!s || !out) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    crt_scene_desc d = s->sm.sceneDesc();
+    int rc = crt_scene_create(&d, device, out);
+    if (rc) g_err = crt_last_error();
+    return rc;
+}
+
+int crth_scene_counts(const crth_scene* s, int64_t* c) {
+    if (!s || !c) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    c[0] = (int64_t)s->sm.meshes().size();
+    c[1] = (int64_t)s->sm.positions().size() / 3;
+    c[2] = (int64_t)s->sm.indices().size();
+    c[3] = (int64_t)s->sm.faceMaterials().size();
+    c[4] = (int64_t)s->sm.sceneMaterialsData().size();
+    return CRT_OK;
+}
+
+int crth_scene_loader_arrays(const crth_scene* s, float* pos, uint32_t* idx, int32_t* fm, uint32_t* info, float* mats) {
+    if (!s) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    const auto& P = s->sm.positions();
+    if (pos) std::memcpy(pos, P.data(), P.size() * sizeof(float));
+    if (idx) std::memcpy(idx, s->idx0.data(), s->idx0.size() * sizeof(uint32_t));
+    if (fm) std::memcpy(fm, s->fmat0.data(), s->fmat0.size() * sizeof(int32_t));
+    if (info) {
+        const auto& M = s->sm.meshes();
+        for (size_t i = 0; i < M.size(); ++i) {
+            uint32_t* o = info + 6 * i;
+            o[0] = M[i].vertex_offset; o[1] = M[i].vertex_count; o[2] = M[i].index_offset;
+            o[3] = M[i].index_count; o[4] = M[i].face_offset; o[5] = M[i].material_id_offset;
+        }
+    }
+    if (mats) {
+        const auto& D = s->sm.sceneMaterialsData();
+        for (size_t i = 0; i < D.size(); ++i) {
+            float* o = mats + 9 * i;
+            o[0] = (float)(int)D[i].getType();
+            for (int c = 0; c < 3; ++c) { o[1 + c] = D[i].getAlbedo()[c]; o[4 + c] = D[i].getEmission()[c]; }
+            o[7] = D[i].getRoughness();
+            o[8] = D[i].getIOR();
+        }
+    }
+    return CRT_OK;
+}
+
+int crth_camera(float aspect, float vfov, const float* pos3, const float* up3, float aperture, float focus,
+                float yaw, float pitch, int spp, crt_camera_desc* out) {
+    if (!pos3 || !up3 || !out || spp <= 0) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    CRT::Camera cam(aspect, vfov, CRT::Vec3(pos3[0], pos3[1], pos3[2]), CRT::Vec3(0, 0, 0),
+                    CRT::Vec3(up3[0], up3[1], up3[2]), aperture, focus);
+    if (yaw != -90.0f || pitch != 0.0f) cam.setYawPitch(yaw, pitch);
+    cam.setSamplesPerPixel(spp);
+    *out = cam.toDesc();
+    return CRT_OK;
+}
+
+}  // extern "C"
