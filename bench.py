@@ -1,0 +1,249 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark: Mrays/s + frame wall-clock, Cornell + bunny,
+2560x1440, 2000 spp, 20 bounces (BASELINE.json `metric`, configs[2]).
+
+One step = one complete frame of the reference render path (CUDAKernels.h:147-166)
+from fresh per-pixel RNG state: initRandState-equivalent + the render kernel +
+(N>1) the RCCL reduce of the fp32 framebuffer + writeColor.  The scene (BVHs,
+triangles, materials) is resident in HBM before the timed region.  N GPUs shard the
+frame's samples (strong scaling: total work per frame is fixed).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+rank 0 prints ONE JSON line (last line of stdout); progress goes to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path[:0] = [str(REPO / "raytracer-cuda_amd"), str(REPO)]
+
+METRIC = "Mrays/sec + frame wall-clock, Cornell+bunny 2560×1440 2000spp 20bounce"
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK_TOPS = 157.3 / 2       # f32 vector: 157.3 TFLOP/s counts an FMA as 2; the path has no FMA
+
+# Algorithmic bytes / FP ops per unit of work:
+B_BOX, B_TRI, B_SPHERE, B_RAY = 32, 36, 20, 16     # node box+link; v0,e1,e2; c,r,r^2; material/hit
+B_PIXEL = 24 + 24 + 12                              # RNG state in + out, fp32 sum out
+F_BOX, F_TRI, F_SPHERE, F_RAY = 24, 54, 30, 100
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="cornell_bunny", choices=["cornell", "cornell_bunny", "cornell_1m"])
+    ap.add_argument("--width", type=int, default=2560)
+    ap.add_argument("--height", type=int, default=1440)
+    ap.add_argument("--spp", type=int, default=2000)
+    ap.add_argument("--bounces", type=int, default=20)
+    ap.add_argument("--seed", type=int, default=41)
+    ap.add_argument("--no-count", action="store_true", help="skip the work-counting launch (roofline -> null)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--save-ppm", default="", help="rank 0 writes the resolved frame here")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, cam_floats, log_fn):
+    """Oracle (C restatement of the reference path, kind 'port') on this host's cores, bounded sample:
+    the full frame at a reduced spp chosen so the run takes about args.cpu_seconds."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import objload
+    import pyoracle
+    from crt_amd import assets
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    threads = max(1, min(16, ncpu))
+    sc = pyoracle.OracleScene(objload.load_scene(assets.scene_files(args.scene)))
+    w, h = args.width, args.height
+    t = time.perf_counter()
+    _, _, c1 = sc.render(cam_floats, w, h, 1, args.bounces, seed=args.seed, nthreads=threads)
+    t1 = time.perf_counter() - t
+    spp = int(max(1, min(64, round(args.cpu_seconds / max(t1, 1e-3)))))
+    if spp > 1:
+        t = time.perf_counter()
+        _, _, c = sc.render(cam_floats, w, h, spp, args.bounces, seed=args.seed, nthreads=threads)
+        dt = time.perf_counter() - t
+    else:
+        c, dt = c1, t1
+    log_fn(f"[cpu] oracle {w}x{h} {spp}spp: {c['rays']} rays in {dt:.2f}s on {threads} threads")
+    return {"value": round(c["rays"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"full {w}x{h} frame, {spp} spp/pixel, {args.bounces} bounces, seed {args.seed} "
+                      f"(same scene + camera as the GPU run; {c['rays']} rays in {dt:.2f} s)",
+            "frame_wall_s_extrapolated": round(dt * args.spp / spp, 1)}
+
+
+def pmc_traffic(workload_key: str):
+    """HBM bytes per render launch from a committed rocprofv3 --pmc summary for this workload (or None)."""
+    p = REPO / "profiles" / "pmc_traffic.json"
+    if not p.exists():
+        return None, None
+    try:
+        d = json.loads(p.read_text())
+        e = d.get(workload_key)
+        return (e["hbm_bytes_per_launch"], e.get("source")) if e else (None, None)
+    except Exception:
+        return None, None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import crt_amd
+    from crt_amd import assets
+    from crt_amd.dist import ShardedFrameRenderer, dist_env
+
+    rank, local, world = dist_env()
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    log_r = log if rank == 0 else (lambda *a: None)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def allreduce_max(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def allreduce_sum_i(xs):
+        if world == 1:
+            return list(xs)
+        t = torch.tensor(list(xs), dtype=torch.int64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return [int(v) for v in t.tolist()]
+
+    W, H = args.width, args.height
+    files = assets.scene_files(args.scene) if rank == 0 else None
+    barrier()
+    files = assets.scene_files(args.scene)
+    t = time.perf_counter()
+    hs = crt_amd.HostScene(files)
+    scene = hs.upload(local)
+    t_scene = time.perf_counter() - t
+    st = scene.stats()
+    counts = hs.counts()
+    log_r(f"[scene] {args.scene}: {counts['n_indices'] // 3} triangles, {st['device_nodes']} nodes, "
+          f"{st['device_bytes'] / 1e6:.1f} MB in HBM, host load+build+upload {t_scene:.2f}s")
+
+    cam = crt_amd.camera(args.spp)
+    r = crt_amd.Renderer(W, H, local)
+    r.set_camera(cam)
+    fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world)
+    log_r(f"[plan] {world} rank(s), spp per rank {[fr.spp] if world == 1 else 'spp/N'}")
+
+    for i in range(args.warmup):
+        t = time.perf_counter()
+        fr.render()
+        torch.cuda.synchronize()
+        log_r(f"[warmup {i}] {time.perf_counter() - t:.3f}s")
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        fr.render(*evs[k])
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = allreduce_max(elapsed)
+    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    kernel_ms_avg = sum(kernel_ms) / len(kernel_ms)
+    kernel_ms_max = allreduce_max(max(kernel_ms))
+    rays_rank = r.counters()["rays"]
+    [rays_frame] = allreduce_sum_i([rays_rank])
+    log_r(f"[timed] {args.steps} frames in {elapsed:.3f}s; render kernel {kernel_ms_avg:.1f} ms avg (rank 0); "
+          f"{rays_frame} rays/frame")
+
+    if args.save_ppm and rank == 0:
+        img = r.rgba8()
+        with open(args.save_ppm, "wb") as f:
+            f.write(b"P6\n%d %d\n255\n" % (W, H))
+            f.write(img[::-1, :, :3].tobytes())
+
+    # exact work counts for the same launch (deterministic: same seed, same shard)
+    roofline = roofline_valu = None
+    work = None
+    if not args.no_count:
+        r.init_rand(args.seed, fr.subseq)
+        r.render(scene, fr.spp, args.bounces, count_work=True)
+        r.synchronize()
+        work = r.counters()
+        assert work["rays"] == rays_rank, "counting kernel disagrees with the timed kernel"
+        bytes_launch = (B_BOX * work["box_tests"] + B_TRI * work["tri_tests"] + B_SPHERE * work["sphere_tests"]
+                        + B_RAY * work["rays"] + B_PIXEL * W * H)
+        flops_launch = (F_BOX * work["box_tests"] + F_TRI * work["tri_tests"] + F_SPHERE * work["sphere_tests"]
+                        + F_RAY * work["rays"])
+        achieved = bytes_launch / (kernel_ms_avg / 1e3) / 1e9
+        wkey = f"{args.scene}_{W}x{H}_{fr.spp}spp_{args.bounces}b"
+        traffic, tsrc = pmc_traffic(wkey)
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "bytes_per_launch": int(bytes_launch), "kernel": "crt_render_kernel<false>",
+                    "kernel_ms_avg": round(kernel_ms_avg, 3),
+                    "per_ray": {"box_tests": round(work["box_tests"] / work["rays"], 3),
+                                "tri_tests": round(work["tri_tests"] / work["rays"], 3),
+                                "sphere_tests": round(work["sphere_tests"] / work["rays"], 3)},
+                    "note": "algorithmic bytes = 32*box + 36*tri + 20*sphere + 16*ray + 60*pixel (DESIGN.md); "
+                            "the scene (%.1f MB) is L2/Infinity-Cache resident, so HBM traffic is far below "
+                            "this" % (st["device_bytes"] / 1e6)
+                            + ("" if traffic is None else f"; traffic from {tsrc}")}
+        valu = flops_launch / (kernel_ms_avg / 1e3) / 1e12
+        roofline_valu = {"bound": "valu", "achieved": round(valu, 2), "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
+                         "frac": round(valu / VALU_PEAK_TOPS, 4), "ops_per_launch": int(flops_launch)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, crt_amd.camera_floats(cam), log)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = rays_frame * args.steps / elapsed / 1e6
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: authored Cornell box OBJ + seeded 69,300-triangle glass bunny-proxy OBJ "
+                    "(the reference git-ignores its assets)",
+            "config": {"workload": f"{args.scene} {W}x{H} {args.spp}spp {args.bounces} bounces (configs[2])"
+                       if args.scene == "cornell_bunny" else f"{args.scene} {W}x{H} {args.spp}spp {args.bounces} bounces",
+                       "width": W, "height": H, "spp": args.spp, "max_bounces": args.bounces, "seed": args.seed,
+                       "triangles": counts["n_indices"] // 3,
+                       "parallelism": f"spp-shard x{world}" + (" + RCCL reduce of fp32 framebuffer" if world > 1 else "")},
+            "frame_wall_s": round(ms_per_step / 1e3, 4),
+            "rays_per_frame": rays_frame,
+            "paths_per_s": round(W * H * args.spp * args.steps / elapsed, 1),
+            "render_kernel_ms_avg": round(kernel_ms_avg, 3), "render_kernel_ms_max_over_ranks": round(kernel_ms_max, 3),
+            "roofline": roofline, "roofline_valu": roofline_valu, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

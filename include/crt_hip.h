@@ -176,6 +176,9 @@ int  crt_renderer_read_rng(crt_renderer* r, uint32_t* host_out);         /* W*H*
 int  crt_renderer_write_linear(crt_renderer* r, const float* host_in);  /* e.g. after a host-side reduce */
 int  crt_renderer_get_counters(crt_renderer* r, crt_work_counters* out);/* of the last render call */
 float* crt_renderer_linear_device_ptr(crt_renderer* r);   /* for RCCL reduce of the framebuffer */
+/* Bind the linear-sum framebuffer to caller-owned device memory of W*H*3 floats on the renderer's
+ * device (e.g. a tensor the caller all-reduces with RCCL); NULL re-binds the internal buffer. */
+int crt_renderer_attach_linear(crt_renderer* r, float* device_ptr);
 uint8_t* crt_renderer_rgba_device_ptr(crt_renderer* r);
 uint32_t* crt_renderer_rng_device_ptr(crt_renderer* r);
 /* Milliseconds of the last render kernel launch(es), measured with HIP events on the launch stream. */

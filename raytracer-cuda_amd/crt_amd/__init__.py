@@ -199,6 +199,11 @@ class Renderer:
     def last_kernel_ms(self) -> float:
         return float(_lib.hip().crt_renderer_last_kernel_ms(self.h))
 
+    def attach_linear(self, device_ptr: int | None):
+        """Render into caller-owned device memory (W*H*3 f32), e.g. a torch tensor to RCCL-reduce."""
+        check(_lib.hip().crt_renderer_attach_linear(self.h, C.c_void_p(device_ptr) if device_ptr else None),
+              "attach_linear")
+
     def linear_device_ptr(self) -> int:
         return int(_lib.hip().crt_renderer_linear_device_ptr(self.h) or 0)
 

@@ -70,6 +70,7 @@ HIP_SYMBOLS = [
     "crt_renderer_synchronize", "crt_renderer_read_linear", "crt_renderer_read_rgba8", "crt_renderer_read_rng",
     "crt_renderer_write_linear", "crt_renderer_get_counters", "crt_renderer_linear_device_ptr",
     "crt_renderer_rgba_device_ptr", "crt_renderer_rng_device_ptr", "crt_renderer_last_kernel_ms",
+    "crt_renderer_attach_linear",
     "crt_selftest_math", "crt_selftest_rng",
 ]
 HOST_SYMBOLS = [
@@ -81,9 +82,25 @@ _hip = None
 _host = None
 
 
+def _bind_single_runtime() -> None:
+    """Import torch before libcrt_hip.so so the process holds ONE HIP runtime.
+
+    PyTorch-ROCm ships its own libamdhip64.so.7 / libhsa-runtime64.so.1; once torch is
+    loaded, libcrt_hip.so's DT_NEEDED entries resolve to those same objects by SONAME, so
+    torch tensors (RCCL framebuffer reduce) and the crt kernels share one device context.
+    Set CRT_NO_TORCH=1 to bind the system ROCm runtime instead (no torch interop)."""
+    if os.environ.get("CRT_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def hip():
     global _hip
     if _hip is None:
+        _bind_single_runtime()
         if not HIP_LIB.exists():
             raise CrtError(f"{HIP_LIB} not built (run `make -C {PKG_ROOT}` or __graft_entry__.build())")
         L = C.CDLL(str(HIP_LIB), mode=C.RTLD_GLOBAL)
@@ -103,6 +120,7 @@ def hip():
             "crt_renderer_get_counters": ([P, P], i32),
             "crt_renderer_linear_device_ptr": ([P], P), "crt_renderer_rgba_device_ptr": ([P], P),
             "crt_renderer_rng_device_ptr": ([P], P), "crt_renderer_last_kernel_ms": ([P], f32),
+            "crt_renderer_attach_linear": ([P, P], i32),
             "crt_selftest_math": ([P, P, i32, P, P], i32),
             "crt_selftest_rng": ([u64, P, i32, i32, P, P], i32),
         }

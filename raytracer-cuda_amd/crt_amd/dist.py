@@ -1,0 +1,102 @@
+"""Samples-per-pixel sharding across GPUs (one process per GPU, torch.distributed over RCCL).
+
+The reference is single-GPU.  The frame shards naturally by
+samples: rank g of N renders every pixel with spp_g samples (remainder to the low
+ranks) from the disjoint RNG subsequence family  pixel + g*W*H  (curand_init's
+2^67-spaced subsequences, CUDAKernels.h:25), producing a fp32 linear-sum
+framebuffer; ONE collective per frame sums the W*H*3 framebuffers (44.2 MB at
+2560x1440) and writeColor runs on the result with scale 1.f/spp_total.
+
+N = 1 is bit-identical to the unsharded reference frame; N > 1 is the same
+estimator with different (independent) samples — parity there is statistical.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+
+def shard_spp(spp_total: int, world: int, rank: int) -> int:
+    base, rem = divmod(int(spp_total), int(world))
+    return base + (1 if rank < rem else 0)
+
+
+def subsequence_base(rank: int, width: int, height: int) -> int:
+    return int(rank) * int(width) * int(height)
+
+
+def shard_plan(spp_total: int, world: int, width: int, height: int):
+    return [dict(rank=r, spp=shard_spp(spp_total, world, r), subsequence_base=subsequence_base(r, width, height))
+            for r in range(world)]
+
+
+def dist_env():
+    """(rank, local_rank, world_size) from torchrun's environment (defaults: single process)."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+class ShardedFrameRenderer:
+    """One rank's share of a frame + the framebuffer reduce.
+
+    The fp32 framebuffer is a torch tensor on this rank's GPU that the HIP kernel
+    writes directly (crt_renderer_attach_linear); the kernel, the collective and the
+    resolve are all enqueued on torch's current stream, so no host sync sits between
+    them.  `reduce_op` is "all_reduce" (every rank holds the frame) or "reduce" (rank 0).
+    """
+
+    def __init__(self, renderer, scene, spp_total: int, max_bounces: int = 20, seed: int = 41,
+                 rank: int = 0, world: int = 1, group=None, reduce_op: str = "reduce", fb_device=None):
+        import torch
+        self.torch = torch
+        self.r = renderer
+        self.scene = scene
+        self.spp_total = int(spp_total)
+        self.max_bounces = int(max_bounces)
+        self.seed = int(seed)
+        self.rank, self.world, self.group = rank, world, group
+        self.reduce_op = reduce_op
+        self.spp = shard_spp(spp_total, world, rank)
+        self.subseq = subsequence_base(rank, renderer.width, renderer.height)
+        self.fb_device = fb_device or f"cuda:{renderer.device}"
+        self.fb = torch.zeros((renderer.height, renderer.width, 3), dtype=torch.float32, device=self.fb_device)
+        renderer.attach_linear(self.fb.data_ptr())
+        from . import pixel_sample_scale
+        self.scale = pixel_sample_scale(self.spp_total)
+
+    def stream_handle(self):
+        if not str(self.fb_device).startswith("cuda"):
+            return None
+        return self.torch.cuda.current_stream().cuda_stream
+
+    def render(self, ev_start=None, ev_end=None):
+        """Fresh RNG + this rank's samples + framebuffer reduce + resolve (rank 0 / all)."""
+        st = self.stream_handle()
+        self.r.init_rand(self.seed, self.subseq, stream=st)
+        if ev_start is not None:
+            ev_start.record()
+        self.r.render(self.scene, self.spp, self.max_bounces, stream=st)
+        if ev_end is not None:
+            ev_end.record()
+        if self.world > 1:
+            import torch.distributed as dist
+            if self.reduce_op == "all_reduce":
+                dist.all_reduce(self.fb, op=dist.ReduceOp.SUM, group=self.group)
+            else:
+                dist.reduce(self.fb, dst=0, op=dist.ReduceOp.SUM, group=self.group)
+        if self.rank == 0 or self.reduce_op == "all_reduce":
+            self.r.resolve(self.scale, stream=st)
+
+    def linear(self) -> np.ndarray:
+        if str(self.fb_device).startswith("cuda"):
+            self.torch.cuda.synchronize(self.r.device)
+        return self.fb.cpu().numpy()
+
+
+def reduce_framebuffers_cpu(fbs):
+    """Reference reduction order used by the gloo tests: sum in rank order (fp32)."""
+    out = np.zeros_like(fbs[0], dtype=np.float32)
+    for f in fbs:
+        out = (out + f).astype(np.float32)
+    return out

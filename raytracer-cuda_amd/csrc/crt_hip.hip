@@ -549,7 +549,8 @@ struct crt_scene {
 struct crt_renderer {
     int device = 0, width = 0, height = 0;
     uint32_t* d_rng = nullptr;
-    float* d_sum = nullptr;
+    float* d_sum = nullptr;       // active linear framebuffer (own or attached)
+    float* d_sum_own = nullptr;
     uint8_t* d_rgba = nullptr;
     uint32_t* d_seq = nullptr;
     unsigned long long* d_counters = nullptr;
@@ -653,12 +654,12 @@ int crt_renderer_create(int width, int height, int device, crt_renderer** out) {
     const auto& tab = seq_tables();
     hipError_t e;
     if ((e = hipMalloc((void**)&R->d_rng, n * 6 * 4)) != hipSuccess ||
-        (e = hipMalloc((void**)&R->d_sum, n * 3 * 4)) != hipSuccess ||
+        (e = hipMalloc((void**)&R->d_sum_own, n * 3 * 4)) != hipSuccess ||
         (e = hipMalloc((void**)&R->d_rgba, n * 4)) != hipSuccess ||
         (e = hipMalloc((void**)&R->d_seq, tab.size() * 4)) != hipSuccess ||
         (e = hipMalloc((void**)&R->d_counters, 8 * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMemcpy(R->d_seq, tab.data(), tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemset(R->d_sum, 0, n * 3 * 4)) != hipSuccess ||
+        (e = hipMemset(R->d_sum_own, 0, n * 3 * 4)) != hipSuccess ||
         (e = hipMemset(R->d_rgba, 0, n * 4)) != hipSuccess ||
         (e = hipMemset(R->d_counters, 0, 8 * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipEventCreate(&R->ev0)) != hipSuccess || (e = hipEventCreate(&R->ev1)) != hipSuccess) {
@@ -666,7 +667,20 @@ int crt_renderer_create(int width, int height, int device, crt_renderer** out) {
         return set_error(e == hipErrorOutOfMemory ? CRT_ERR_OUT_OF_MEMORY : CRT_ERR_HIP,
                          std::string("renderer allocation: ") + hipGetErrorString(e));
     }
+    R->d_sum = R->d_sum_own;
     *out = R;
+    return CRT_OK;
+}
+
+int crt_renderer_attach_linear(crt_renderer* R, float* ptr) {
+    if (!R) return set_error(CRT_ERR_INVALID_ARGUMENT, "null renderer");
+    if (ptr) {
+        hipPointerAttribute_t attr;
+        HIP_TRY(hipPointerGetAttributes(&attr, ptr));
+        if (attr.type != hipMemoryTypeDevice || attr.device != R->device)
+            return set_error(CRT_ERR_INVALID_ARGUMENT, "attach_linear: not device memory of the renderer's device");
+    }
+    R->d_sum = ptr ? ptr : R->d_sum_own;
     return CRT_OK;
 }
 
@@ -674,7 +688,7 @@ void crt_renderer_destroy(crt_renderer* R) {
     if (!R) return;
     (void)hipSetDevice(R->device);
     if (R->d_rng) (void)hipFree(R->d_rng);
-    if (R->d_sum) (void)hipFree(R->d_sum);
+    if (R->d_sum_own) (void)hipFree(R->d_sum_own);
     if (R->d_rgba) (void)hipFree(R->d_rgba);
     if (R->d_seq) (void)hipFree(R->d_seq);
     if (R->d_counters) (void)hipFree(R->d_counters);

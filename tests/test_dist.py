@@ -1,0 +1,100 @@
+"""spp sharding + framebuffer reduce, exercised on CPU with torch.distributed gloo (world 2).
+
+The rank-local 'renderer' is the oracle (a stand-in for the HIP kernel, which needs a
+GPU); ShardedFrameRenderer, the shard plan and the collective are the production code.
+"""
+import ctypes as C
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from crt_amd.dist import ShardedFrameRenderer, reduce_framebuffers_cpu, shard_plan, shard_spp, subsequence_base
+
+W, H, SPP = 24, 16, 5
+
+
+def test_shard_plan_properties():
+    for spp in (1, 5, 2000):
+        for n in (1, 2, 3, 4, 8):
+            plan = shard_plan(spp, n, 2560, 1440)
+            assert sum(p["spp"] for p in plan) == spp
+            assert max(p["spp"] for p in plan) - min(p["spp"] for p in plan) <= 1
+            bases = [p["subsequence_base"] for p in plan]
+            assert bases == [r * 2560 * 1440 for r in range(n)]   # disjoint 2^67-spaced families
+    assert shard_spp(2000, 8, 0) == 250 and subsequence_base(3, 10, 10) == 300
+
+
+class OracleShardRenderer:
+    """Duck-types crt_amd.Renderer for the calls ShardedFrameRenderer makes."""
+
+    def __init__(self, oscene, cam, w, h):
+        self.o, self.cam, self.width, self.height, self.device = oscene, cam, w, h, 0
+        self.ptr = None
+        self.resolved = None
+
+    def attach_linear(self, ptr):
+        self.ptr = ptr
+
+    def init_rand(self, seed, subseq, stream=None):
+        self.seed, self.subseq = seed, subseq
+
+    def render(self, scene, spp, bounces, stream=None):
+        s, _, _ = self.o.render(self.cam, self.width, self.height, spp, bounces, seed=self.seed,
+                                subseq_base=self.subseq, nthreads=2)
+        C.memmove(self.ptr, s.ctypes.data, s.nbytes)
+
+    def resolve(self, scale, stream=None):
+        self.resolved = scale
+
+
+def _worker(rank, world, port, files, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import objload
+    import pyoracle
+    o = pyoracle.OracleScene(objload.load_scene(files))
+    r = OracleShardRenderer(o, pyoracle.camera(), W, H)
+    fr = ShardedFrameRenderer(r, None, SPP, 20, 41, rank, world, reduce_op="all_reduce", fb_device="cpu")
+    fr.render()
+    q.put((rank, fr.spp, fr.subseq, fr.linear(), r.resolved))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_gloo_world2_sharded_frame(scenes):
+    import objload
+    import pyoracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, scenes["cornell"], q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in ps], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [3, 2]
+    assert [r[2] for r in res] == [0, W * H]
+    # every rank holds the same reduced frame, equal to the sum of the independent shard renders
+    o = pyoracle.OracleScene(objload.load_scene(scenes["cornell"]))
+    parts = [o.render(pyoracle.camera(), W, H, sp, 20, subseq_base=sb)[0] for (_, sp, sb, _, _) in res]
+    ref = reduce_framebuffers_cpu(parts)
+    for r in res:
+        assert np.allclose(r[3], ref, rtol=0, atol=1e-5)
+        assert r[4] == np.float32(1) / np.float32(SPP)
+    # N=1 plan is the unsharded frame (bit-exact)
+    s1 = o.render(pyoracle.camera(), W, H, SPP, 20)[0]
+    assert not np.array_equal(s1, ref)      # different samples ...
+    mean_diff = abs(float(s1.mean() - ref.mean())) / SPP
+    assert mean_diff < 0.05                 # ... same estimator

@@ -133,3 +133,35 @@ def test_full_size_frame_sampled_pixels(device_scenes, oracle_scenes):
     for (x0, y0, x1, y1) in [(0, 0, 64, 4), (1200, 700, 1296, 708), (2496, 1436, 2560, 1440), (1700, 900, 1760, 960)]:
         o_sum, o_rgba, _ = oracle_scenes["cornell_bunny"].render(cf, w, h, spp, 20, rect=(x0, y0, x1, y1))
         _assert_parity(lin[y0:y1, x0:x1], r.rgba8()[y0:y1, x0:x1], o_sum, o_rgba, spp)
+
+
+def test_sharded_n1_is_reference_frame_and_shards_sum(device_scenes):
+    """ShardedFrameRenderer with world=1 (torch framebuffer, torch stream) == plain render, bit-exact;
+    two shards rendered on one GPU and summed == the 2-GPU frame's framebuffer definition."""
+    import torch
+    from crt_amd.dist import ShardedFrameRenderer
+    w, h, spp = 128, 72, 6
+    _, dev = device_scenes["cornell_bunny"]
+    cam = crt_amd.camera(spp)
+    ref = _render(dev, w, h, spp, 20, cam=cam)
+    r = crt_amd.Renderer(w, h)
+    r.set_camera(cam)
+    fr = ShardedFrameRenderer(r, dev, spp, 20, 41, 0, 1)
+    fr.render()
+    torch.cuda.synchronize()
+    assert np.array_equal(fr.linear().view(np.uint32), ref.linear().view(np.uint32))
+    assert np.array_equal(r.rgba8(), ref.rgba8())
+    # shard g of N renders spp_g samples from subsequences pixel + g*W*H: check against the oracle
+    import pyoracle, objload
+    from crt_amd import assets
+    from crt_amd.dist import shard_plan
+    o = pyoracle.OracleScene(objload.load_scene(assets.scene_files("cornell_bunny")))
+    for p in shard_plan(spp, 2, w, h):
+        rr = crt_amd.Renderer(w, h)
+        rr.set_camera(cam)
+        rr.init_rand(41, p["subsequence_base"])
+        rr.render(dev, p["spp"], 20)
+        rr.synchronize()
+        o_sum = o.render(crt_amd.camera_floats(cam), w, h, p["spp"], 20, subseq_base=p["subsequence_base"],
+                         rect=(0, 0, w, 8))[0]
+        assert np.array_equal(rr.linear()[:8].view(np.uint32), o_sum.view(np.uint32))
