@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=41)
     ap.add_argument("--no-count", action="store_true", help="skip the work-counting launch (roofline -> null)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--cpu-seconds", type=float, default=25.0, help="target CPU-baseline sample duration")
     ap.add_argument("--save-ppm", default="", help="rank 0 writes the resolved frame here")
     return ap.parse_args()
 

@@ -165,3 +165,12 @@ def test_sharded_n1_is_reference_frame_and_shards_sum(device_scenes):
         o_sum = o.render(crt_amd.camera_floats(cam), w, h, p["spp"], 20, subseq_base=p["subsequence_base"],
                          rect=(0, 0, w, 8))[0]
         assert np.array_equal(rr.linear()[:8].view(np.uint32), o_sum.view(np.uint32))
+
+
+def test_golden_fixture_frame(device_scenes):
+    """HIP output == the committed oracle fixture (tests/golden, make_golden.py), no live oracle."""
+    from pathlib import Path
+    g = np.load(Path(__file__).resolve().parent / "golden" / "cornell_bunny_64x36_16spp.npz")
+    _, dev = device_scenes["cornell_bunny"]
+    r = _render(dev, 64, 36, 16, 20, cam=crt_amd.camera(16))
+    _assert_parity(r.linear(), r.rgba8(), g["sum"], g["rgba"], 16)
