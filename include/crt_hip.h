@@ -162,6 +162,15 @@ void crt_renderer_destroy(crt_renderer* r);
  * subsequence_base = shard * width * height for spp sharding. */
 int  crt_renderer_init_rand(crt_renderer* r, unsigned long long seed, unsigned long long subsequence_base, void* stream);
 int  crt_renderer_set_camera(crt_renderer* r, const crt_camera_desc* cam);
+/* Render-kernel variant (identical results, different wave scheduling): 0 = per-lane BVH traversal
+ * with per-lane leaf loops; 1 = per-lane traversal with wave-cooperative leaf intersection;
+ * 2 = 1 + traversal-step scheduling with parked-lane regeneration (lanes start their next ray
+ * without waiting for the wave's slowest trace). */
+int  crt_renderer_set_kernel_variant(crt_renderer* r, int variant);
+/* Variant 2: number of parked lanes (1..64, default 32) that triggers a shading/regeneration pass. */
+int  crt_renderer_set_regen_threshold(crt_renderer* r, int lanes);
+/* Variant 2: register-allocation occupancy target in waves per SIMD (1 = compiler default, 5, 6, 8). */
+int  crt_renderer_set_occupancy_target(crt_renderer* r, int waves_per_simd);
 /* Trace `spp` samples per pixel continuing each pixel's RNG stream; the per-pixel
  * linear sum (pixel_color, CUDAKernels.h:157-162) is kept in an fp32 W*H*3 buffer. */
 int  crt_renderer_render(crt_renderer* r, const crt_scene* scene, int spp, int max_bounces, unsigned flags, void* stream);
@@ -175,6 +184,10 @@ int  crt_renderer_read_rgba8(crt_renderer* r, uint8_t* host_out);        /* W*H*
 int  crt_renderer_read_rng(crt_renderer* r, uint32_t* host_out);         /* W*H*6 words: v[5], d */
 int  crt_renderer_write_linear(crt_renderer* r, const float* host_in);  /* e.g. after a host-side reduce */
 int  crt_renderer_get_counters(crt_renderer* r, crt_work_counters* out);/* of the last render call */
+/* Scheduling diagnostics of the last CRT_RENDER_COUNT_WORK render (kernel variant 1), read by
+ * crt_renderer_get_counters: [0] lane-slots of traversal steps (compare box_tests), [1] lane-slots
+ * of cooperative leaf rounds (compare tri_tests), [2] wave-level trace calls. */
+int  crt_renderer_get_schedule_stats(crt_renderer* r, unsigned long long* out3);
 float* crt_renderer_linear_device_ptr(crt_renderer* r);   /* for RCCL reduce of the framebuffer */
 /* Bind the linear-sum framebuffer to caller-owned device memory of W*H*3 floats on the renderer's
  * device (e.g. a tensor the caller all-reduces with RCCL); NULL re-binds the internal buffer. */
@@ -188,6 +201,9 @@ float crt_renderer_last_kernel_ms(crt_renderer* r);
 /* For n inputs a[i], b[i] (f32) computes on the device: a/b, sqrtf(|a|), 1/a, (double)sqrt((double)|a|)
  * into out[4*i..4*i+3] (the last one converted to float bits as a double->float cast). */
 int crt_selftest_math(const float* a, const float* b, int n, float* out, double* out_f64);
+/* Wave64 scan self-test: for n_waves x 64 ints, out[3*i..] = DPP inclusive sum, ds_bpermute inclusive sum,
+ * DPP inclusive max (per wave of 64 consecutive entries). */
+int crt_selftest_scan(const int* in, int n_waves, int* out);
 /* XORWOW device self-test: init(seed, subseq[i]) then n_draw uniforms per entry. */
 int crt_selftest_rng(unsigned long long seed, const unsigned long long* subseq, int n, int n_draw,
                      uint32_t* state_out /* n*6 */, float* uniforms_out /* n*n_draw */);

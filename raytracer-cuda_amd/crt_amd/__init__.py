@@ -158,6 +158,15 @@ class Renderer:
     def init_rand(self, seed: int = 41, subsequence_base: int = 0, stream=None):
         check(_lib.hip().crt_renderer_init_rand(self.h, int(seed), int(subsequence_base), stream), "init_rand")
 
+    def set_kernel_variant(self, variant: int):
+        check(_lib.hip().crt_renderer_set_kernel_variant(self.h, int(variant)), "set_kernel_variant")
+
+    def set_occupancy_target(self, waves_per_simd: int):
+        check(_lib.hip().crt_renderer_set_occupancy_target(self.h, int(waves_per_simd)), "set_occupancy_target")
+
+    def set_regen_threshold(self, lanes: int):
+        check(_lib.hip().crt_renderer_set_regen_threshold(self.h, int(lanes)), "set_regen_threshold")
+
     def set_camera(self, cam: CameraDesc):
         self._cam = cam
         check(_lib.hip().crt_renderer_set_camera(self.h, C.byref(cam)), "set_camera")
@@ -195,6 +204,12 @@ class Renderer:
         w = WorkCounters()
         check(_lib.hip().crt_renderer_get_counters(self.h, C.byref(w)), "get_counters")
         return {k: int(getattr(w, k)) for k, _ in WorkCounters._fields_}
+
+    def schedule_stats(self) -> dict:
+        """Lane-slot diagnostics of the last counting render (see crt_renderer_get_schedule_stats)."""
+        a = (C.c_ulonglong * 3)()
+        check(_lib.hip().crt_renderer_get_schedule_stats(self.h, a), "get_schedule_stats")
+        return {"step_lane_slots": int(a[0]), "round_lane_slots": int(a[1]), "wave_trace_calls": int(a[2])}
 
     def last_kernel_ms(self) -> float:
         return float(_lib.hip().crt_renderer_last_kernel_ms(self.h))

@@ -70,8 +70,9 @@ HIP_SYMBOLS = [
     "crt_renderer_synchronize", "crt_renderer_read_linear", "crt_renderer_read_rgba8", "crt_renderer_read_rng",
     "crt_renderer_write_linear", "crt_renderer_get_counters", "crt_renderer_linear_device_ptr",
     "crt_renderer_rgba_device_ptr", "crt_renderer_rng_device_ptr", "crt_renderer_last_kernel_ms",
-    "crt_renderer_attach_linear",
-    "crt_selftest_math", "crt_selftest_rng",
+    "crt_renderer_attach_linear", "crt_renderer_set_kernel_variant", "crt_renderer_get_schedule_stats",
+    "crt_renderer_set_regen_threshold", "crt_renderer_set_occupancy_target",
+    "crt_selftest_math", "crt_selftest_rng", "crt_selftest_scan",
 ]
 HOST_SYMBOLS = [
     "crth_scene_load", "crth_scene_destroy", "crth_scene_desc", "crth_scene_upload", "crth_scene_counts",
@@ -121,8 +122,13 @@ def hip():
             "crt_renderer_linear_device_ptr": ([P], P), "crt_renderer_rgba_device_ptr": ([P], P),
             "crt_renderer_rng_device_ptr": ([P], P), "crt_renderer_last_kernel_ms": ([P], f32),
             "crt_renderer_attach_linear": ([P, P], i32),
+            "crt_renderer_set_kernel_variant": ([P, i32], i32),
+            "crt_renderer_get_schedule_stats": ([P, P], i32),
+            "crt_renderer_set_regen_threshold": ([P, i32], i32),
+            "crt_renderer_set_occupancy_target": ([P, i32], i32),
             "crt_selftest_math": ([P, P, i32, P, P], i32),
             "crt_selftest_rng": ([u64, P, i32, i32, P, P], i32),
+            "crt_selftest_scan": ([P, i32, P], i32),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)

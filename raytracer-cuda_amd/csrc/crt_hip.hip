@@ -41,16 +41,18 @@ struct RenderParams {
     const float4* __restrict__ nodes;
     const float4* __restrict__ prims;
     const float4* __restrict__ mats;
-    int n_nodes, n_mats;
+    int n_nodes, n_mats, n_prims;
+    unsigned* err;                // device error flag (bit 0: primitive index out of range)
     int width, height, spp, max_bounces;
     int accumulate;
+    int regen_threshold;          // variant 2: parked lanes needed before a shading/regeneration pass
     uint32_t* __restrict__ rng;   // W*H*6 (v0..v4, d)
     float* __restrict__ sum;      // W*H*3
     unsigned long long* __restrict__ counters;  // crt_work_counters layout
     crt_camera_desc cam;
 };
 
-struct TraceCounts { uint32_t boxes, tris, spheres; };
+struct TraceCounts { uint32_t boxes, tris, spheres, step_slots, round_slots, trace_calls; };
 
 // Closest hit over the threaded scene+mesh BVH.  Returns hit prim (SPHERE_BIT set for
 // spheres) or -1; `closest` = IntersectionTime of the accepted hit.
@@ -139,8 +141,416 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
     return x;
 }
 
+// ---------------------------------------------------------------- wave helpers
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// Wave64 inclusive scans with DPP (no LDS traffic): Kogge-Stone inside each 16-lane row
+// (row_shr 1,2,4,8 with identity fill), then row_bcast15 / row_bcast31 carry the row totals.
+// Same sequence as LLVM's AMDGPU atomic optimizer uses on gfx9.
+#define CRT_DPP_ROW_SHR(n) (0x110 | (n))
+#define CRT_DPP_BCAST15 0x142
+#define CRT_DPP_BCAST31 0x143
+__device__ __forceinline__ int wave_inclusive_scan(int x, int /*lane*/) {
+    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_ROW_SHR(1), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_ROW_SHR(2), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_ROW_SHR(4), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_ROW_SHR(8), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_BCAST15, 0xa, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_BCAST31, 0xc, 0xf, false);
+    return x;
+}
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+__device__ __forceinline__ int wave_inclusive_max_scan(int x, int /*lane*/) {
+    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, CRT_DPP_ROW_SHR(1), 0xf, 0xf, false));
+    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, CRT_DPP_ROW_SHR(2), 0xf, 0xf, false));
+    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, CRT_DPP_ROW_SHR(4), 0xf, 0xf, false));
+    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, CRT_DPP_ROW_SHR(8), 0xf, 0xf, false));
+    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, CRT_DPP_BCAST15, 0xa, 0xf, false));
+    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, CRT_DPP_BCAST31, 0xc, 0xf, false));
+    return x;
+}
+// Reference (ds_bpermute) form, used by the scan self-test.
+__device__ __forceinline__ int wave_inclusive_scan_shfl(int x, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    return x;
+}
+
+// Per-wave LDS for the cooperative leaf step.
+struct WaveLds {
+    float4 ray0[64];                 // o.x, o.y, o.z, d.x of each lane's ray
+    float4 ray1[64];                 // d.y, d.z, closest at leaf entry, first prim (int bits)
+    unsigned long long key[64];      // per owner: (t bits << 32) | (0xffffffff - k), min-reduced
+    int prefix[64];                  // first pair index of each owner's leaf
+    unsigned char owner_at[64];      // owner lane of the pair that starts at each slot of a round
+};
+
+// Möller–Trumbore (Mesh.cuh:266-308) on prim p; returns t or -1 when rejected (any accepted t >= 0.001).
+__device__ __forceinline__ float tri_test(const float4* __restrict__ prims, int p, V3 o, V3 d, float tmax) {
+    const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1], f2 = prims[3 * p + 2];
+    const V3 e1 = v3(f0.w, f1.x, f1.y);
+    const V3 e2 = v3(f1.z, f1.w, f2.x);
+    const V3 h = cross(d, e2);
+    const float det = dot(e1, h);
+    if (fabsf(det) < 1e-8f) return -1.f;
+    const float f = 1.f / det;
+    const V3 s = o - v3(f0.x, f0.y, f0.z);
+    const float u = f * dot(s, h);
+    if (u < 0.f || u > 1.f) return -1.f;
+    const V3 q = cross(s, e1);
+    const float v = f * dot(d, q);
+    if (v < 0.f || (u + v) > 1.f) return -1.f;
+    const float t = f * dot(e2, q);
+    if (t < 0.001f || t > tmax) return -1.f;
+    return t;
+}
+
+// Sphere::hit (Sphere.cuh:27-47) against [0.001, closest]; updates closest/hit on acceptance.
+__device__ __forceinline__ void sphere_test(const float4* __restrict__ prims, int b, V3 o, V3 d, float& closest, int& hit) {
+    const int p = b - SPHERE_BIT;
+    const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1];
+    const V3 oc = o - v3(f0.x, f0.y, f0.z);
+    const float qa = dot(d, d);
+    const float hb = dot(oc, d);
+    const float qc = dot(oc, oc) - f1.x;
+    const float disc = hb * hb - qa * qc;
+    if (disc < 0) return;
+    const float sq = sqrtf(disc);
+    float root = (-hb - sq) / qa;
+    if (root < 0.001f || root > closest) {
+        root = (-hb + sq) / qa;
+        if (root < 0.001f || root > closest) return;
+    }
+    closest = root;
+    hit = b;
+}
+
+// Variant 1: per-lane threaded traversal, leaf triangles tested cooperatively by the whole wave.
+// Every lane that reaches a mesh leaf in a step contributes its (lane, triangle) pairs; the wave
+// tests 64 pairs per round and min-reduces (t, later-index-wins) per owner in LDS.  Within one
+// leaf a triangle's acceptance depends only on the closest hit at leaf entry, so the result is
+// the same closest hit (ties to the later triangle) as Mesh::hit's sequential loop.
+// MUST be called by all 64 lanes (inactive lanes pass active=false).
 template <bool COUNT>
-__global__ __launch_bounds__(256) void crt_render_kernel(RenderParams P) {
+__device__ int trace_coop(const float4* __restrict__ nodes, const float4* __restrict__ prims, int n_nodes,
+                          int n_prims, unsigned* err, V3 o, V3 d, bool active, float& closest, TraceCounts& cnt,
+                          WaveLds& L, int lane) {
+    const float INF = __builtin_inff();
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    closest = INF;
+    int hit = -1;
+    int node = active ? 0 : n_nodes;
+    L.ray0[lane] = make_float4(o.x, o.y, o.z, d.x);
+    L.owner_at[lane] = 0xff;
+    if (COUNT) cnt.trace_calls++;
+    while (__ballot(node < n_nodes)) {
+        if (COUNT) cnt.step_slots++;        // one traversal step of the wave (x64 lanes)
+        int leaf_n = 0, leaf_first = 0;
+        if (node < n_nodes) {
+            const float4 A = nodes[2 * node];
+            const float4 B = nodes[2 * node + 1];
+            const int a = __float_as_int(B.z);
+            const int b = __float_as_int(B.w);
+            const bool scene_level = (b == NODE_SCENE_INNER) || (b >= SPHERE_BIT);
+            const float tcl = scene_level ? INF : closest;
+            if (COUNT) cnt.boxes++;
+            const float t0x = (A.x - o.x) * inv.x, t0y = (A.y - o.y) * inv.y, t0z = (A.z - o.z) * inv.z;
+            const float t1x = (A.w - o.x) * inv.x, t1y = (B.x - o.y) * inv.y, t1z = (B.y - o.z) * inv.z;
+            float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+            float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+            tmin = fmaxf(tmin, 0.001f);
+            tmax = fminf(tmax, tcl);
+            const bool box_hit = !(tmax <= tmin);
+            int next = node + 1;
+            if (b < 0) {
+                if (!box_hit) next = a;
+            } else if (box_hit) {
+                if (b >= SPHERE_BIT) {
+                    if (COUNT) cnt.spheres++;
+                    sphere_test(prims, b, o, d, closest, hit);
+                } else {
+                    leaf_n = a;
+                    leaf_first = b;
+                }
+            }
+            node = next;
+        }
+        if (!__ballot(leaf_n > 0)) continue;
+        const int incl = wave_inclusive_scan(leaf_n, lane);
+        const int total = __builtin_amdgcn_readlane(incl, 63);
+        const int pfx = incl - leaf_n;
+        if (leaf_n > 0) {
+            L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first));
+            L.prefix[lane] = pfx;
+            L.key[lane] = ~0ull;
+        }
+        int carry = 0;
+        for (int base = 0; base < total; base += 64) {
+            if (COUNT) cnt.round_slots++;
+            // owner of pair (base + lane): lanes whose leaf starts in this round mark their start slot,
+            // then an inclusive max-scan over slots (owners are increasing in slot order) fills the gaps;
+            // slots before the first start of the round belong to the previous round's last owner.
+            if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)lane;
+            wave_sync();
+            const int mark = L.owner_at[lane];
+            L.owner_at[lane] = 0xff;                  // reset own slot for the next round
+            int owner = wave_inclusive_max_scan(mark == 0xff ? -1 : mark, lane);
+            owner = owner > carry ? owner : carry;
+            const int j = base + lane;
+            if (j < total) {
+                const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
+                const int k = j - L.prefix[owner];
+                const int p = __float_as_int(r1.w) + k;
+                if (COUNT) cnt.tris++;
+                if ((unsigned)p < (unsigned)n_prims && (unsigned)k < 0xffffffffu) {
+                    const float t = tri_test(prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z);
+                    if (t >= 0.f)
+                        atomicMin(&L.key[owner], ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)k));
+                } else {
+                    atomicOr(err, 1u);                // indexing bug: report instead of faulting
+                }
+            }
+            carry = __builtin_amdgcn_readlane(owner, 63);
+            wave_sync();
+        }
+        if (leaf_n > 0) {
+            const unsigned long long kk = L.key[lane];
+            if (kk != ~0ull) {
+                closest = __uint_as_float((unsigned)(kk >> 32));
+                hit = leaf_first + (int)(0xffffffffu - (unsigned)kk);
+            }
+        }
+    }
+    return hit;
+}
+
+// One wave traversal step (variant 2): every lane with node < n_nodes tests one node; the leaves
+// reached in this step are intersected cooperatively (same rounds as trace_coop).  All 64 lanes call it.
+template <bool COUNT>
+__device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
+                                              int n_nodes, int n_prims, unsigned* err, V3 o, V3 d, V3 inv,
+                                              int& node, float& closest, int& hit, TraceCounts& cnt, WaveLds& L,
+                                              int lane) {
+    const float INF = __builtin_inff();
+    if (COUNT) cnt.step_slots++;
+    int leaf_n = 0, leaf_first = 0;
+    if (node < n_nodes) {
+        const float4 A = nodes[2 * node];
+        const float4 B = nodes[2 * node + 1];
+        const int a = __float_as_int(B.z);
+        const int b = __float_as_int(B.w);
+        const bool scene_level = (b == NODE_SCENE_INNER) || (b >= SPHERE_BIT);
+        const float tcl = scene_level ? INF : closest;
+        if (COUNT) cnt.boxes++;
+        const float t0x = (A.x - o.x) * inv.x, t0y = (A.y - o.y) * inv.y, t0z = (A.z - o.z) * inv.z;
+        const float t1x = (A.w - o.x) * inv.x, t1y = (B.x - o.y) * inv.y, t1z = (B.y - o.z) * inv.z;
+        float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+        float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+        tmin = fmaxf(tmin, 0.001f);
+        tmax = fminf(tmax, tcl);
+        const bool box_hit = !(tmax <= tmin);
+        int next = node + 1;
+        if (b < 0) {
+            if (!box_hit) next = a;
+        } else if (box_hit) {
+            if (b >= SPHERE_BIT) {
+                if (COUNT) cnt.spheres++;
+                sphere_test(prims, b, o, d, closest, hit);
+            } else {
+                leaf_n = a;
+                leaf_first = b;
+            }
+        }
+        node = next;
+    }
+    if (!__ballot(leaf_n > 0)) return;
+    const int incl = wave_inclusive_scan(leaf_n, lane);
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    const int pfx = incl - leaf_n;
+    if (leaf_n > 0) {
+        L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first));
+        L.prefix[lane] = pfx;
+        L.key[lane] = ~0ull;
+    }
+    int carry = 0;
+    for (int base = 0; base < total; base += 64) {
+        if (COUNT) cnt.round_slots++;
+        if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)lane;
+        wave_sync();
+        const int mark = L.owner_at[lane];
+        L.owner_at[lane] = 0xff;
+        int owner = wave_inclusive_max_scan(mark == 0xff ? -1 : mark, lane);
+        owner = owner > carry ? owner : carry;
+        const int j = base + lane;
+        if (j < total) {
+            const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
+            const int k = j - L.prefix[owner];
+            const int p = __float_as_int(r1.w) + k;
+            if (COUNT) cnt.tris++;
+            if ((unsigned)p < (unsigned)n_prims) {
+                const float t = tri_test(prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z);
+                if (t >= 0.f)
+                    atomicMin(&L.key[owner], ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)k));
+            } else {
+                atomicOr(err, 1u);
+            }
+        }
+        carry = __builtin_amdgcn_readlane(owner, 63);
+        wave_sync();
+    }
+    if (leaf_n > 0) {
+        const unsigned long long kk = L.key[lane];
+        if (kk != ~0ull) {
+            closest = __uint_as_float((unsigned)(kk >> 32));
+            hit = leaf_first + (int)(0xffffffffu - (unsigned)kk);
+        }
+    }
+}
+
+// Per-lane path state of one pixel (rayColor's locals, CUDAKernels.h:102-145, plus the sample loop).
+struct PathState {
+    Rng s;
+    V3 pixel, o, d, thr;
+    int remaining, bounce;
+    bool need_new;
+    uint32_t rays, paths;
+};
+
+struct CamRegs {
+    V3 pos, llc, hor, ver, right, up;
+    float lens, fw, fh;
+};
+
+// Phase 1: give the lane a ray to trace — Camera::getRay for a new sample, the bounce-limit exit and
+// Russian roulette (CUDAKernels.h:110-121).  Returns false when the pixel has no samples left.
+__device__ __forceinline__ bool next_ray(PathState& S, const CamRegs& C, int x, int y, int max_bounces) {
+    for (;;) {
+        if (S.need_new) {
+            if (S.remaining == 0) return false;
+            --S.remaining;
+            float da, db;                                    // Utility::randomPointInUnitDisk
+            for (;;) {
+                da = rand_pm1(S.s);
+                db = rand_pm1(S.s);
+                if (len2(v3(da, db, 0)) >= 1) continue;
+                break;
+            }
+            const V3 rd = C.lens * v3(da, db, 0);
+            const V3 off = v3(C.right.x * rd.x, C.right.y * rd.x, C.right.z * rd.x) +
+                           v3(C.up.x * rd.y, C.up.y * rd.y, C.up.z * rd.y);
+            const float u = ((float)x + uniform(S.s)) / C.fw;
+            const float v = ((float)y + uniform(S.s)) / C.fh;
+            S.o = C.pos + off;
+            S.d = (((C.llc + u * C.hor) + v * C.ver) - C.pos) - off;
+            S.thr = v3(1.0f, 1.0f, 1.0f);
+            S.bounce = 0;
+            S.need_new = false;
+        }
+        if (S.bounce >= max_bounces) {                      // loop exhausted: final_color = 0
+            S.pixel = S.pixel + v3(0.0f, 0.0f, 0.0f);
+            ++S.paths;
+            S.need_new = true;
+            continue;
+        }
+        if (S.bounce >= 3) {
+            float p = fmaxf(S.thr.x, fmaxf(S.thr.y, S.thr.z));
+            p = fminf(p, 0.95f);
+            if (uniform(S.s) > p) {
+                S.pixel = S.pixel + v3(0.0f, 0.0f, 0.0f);
+                ++S.paths;
+                S.need_new = true;
+                continue;
+            }
+            S.thr = (1 / p) * S.thr;
+        }
+        return true;
+    }
+}
+
+// Phase 3: material scatter / emit / sky (CUDAKernels.h:123-142, Material.cuh:66-146).
+__device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int hit, float t) {
+    if (hit < 0) {                                       // :137-142
+        S.pixel = S.pixel + S.thr * sky(S.d);
+        ++S.paths;
+        S.need_new = true;
+        return;
+    }
+    const V3 hp = S.o + t * S.d;                         // Ray::pointAtDistance
+    V3 outward;
+    uint32_t mat;
+    if (hit >= SPHERE_BIT) {
+        const int p = hit - SPHERE_BIT;
+        const float4 f0 = P.prims[3 * p], f1 = P.prims[3 * p + 1];
+        outward = (1 / f0.w) * (hp - v3(f0.x, f0.y, f0.z));   // Sphere.cuh:44
+        mat = (uint32_t)__float_as_int(f1.y);
+    } else {
+        const float4 f0 = P.prims[3 * hit], f1 = P.prims[3 * hit + 1], f2 = P.prims[3 * hit + 2];
+        outward = unit(cross(v3(f0.w, f1.x, f1.y), v3(f1.z, f1.w, f2.x)));   // Mesh.cuh:303-304
+        mat = (uint32_t)__float_as_int(f2.y);
+    }
+    const bool front = dot(S.d, outward) < 0;            // HitInfo::setFaceNormal
+    const V3 n = front ? outward : -outward;
+    if (!(mat < (uint32_t)P.n_mats)) {                   // :127 invalid material: same ray again
+        ++S.bounce;
+        return;
+    }
+    const float4 m0 = P.mats[3 * mat], m1 = P.mats[3 * mat + 1];
+    const int mtype = __float_as_int(m0.x);
+    if (mtype == CRT_LAMBERTIAN) {                       // Material.cuh:66-77
+        V3 sd = n + rand_unit_vector(S.s);
+        if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = n;
+        S.thr = S.thr * v3(m0.y, m0.z, m0.w);
+        S.o = hp;
+        S.d = sd;
+        ++S.bounce;
+    } else if (mtype == CRT_METAL) {                     // :89-96
+        V3 refl = reflect(S.d, n);
+        refl = unit(refl) + (m1.w * rand_unit_vector(S.s));
+        if (dot(refl, n) > 0) {
+            S.thr = S.thr * v3(m0.y, m0.z, m0.w);
+            S.o = hp;
+            S.d = refl;
+            ++S.bounce;
+        } else {                                         // absorbed: return Material::emit() = 0
+            S.pixel = S.pixel + v3(0.0f, 0.0f, 0.0f);
+            ++S.paths;
+            S.need_new = true;
+        }
+    } else if (mtype == CRT_DIELECTRIC) {                // :109-128
+        const float ior = P.mats[3 * mat + 2].x;
+        const float ri = front ? (1.0f / ior) : ior;
+        const V3 ud = unit(S.d);
+        const double cos_theta = fminf(dot(-ud, n), 1.0f);
+        const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+        const bool cannot_refract = (double)ri * sin_theta > 1.0;
+        V3 dir;
+        if (cannot_refract || schlick((float)cos_theta, ri) > uniform(S.s))
+            dir = reflect(ud, n);
+        else
+            dir = refract(ud, n, ri);
+        S.o = hp;
+        S.d = dir;
+        ++S.bounce;   // attenuation (1,1,1): thr unchanged (x*1 == x)
+    } else {                                             // DiffuseLight: return emit() raw
+        const V3 em = (mtype == CRT_DIFFUSE_LIGHT) ? v3(m1.x, m1.y, m1.z) : v3(0.0f, 0.0f, 0.0f);
+        S.pixel = S.pixel + em;
+        ++S.paths;
+        S.need_new = true;
+    }
+}
+
+// VARIANT 0: per-lane traversal (leaf loops inside the lane).  VARIANT 1: cooperative leaves.
+// VARIANT 2: cooperative leaves + traversal-step scheduling.  MINW: occupancy target (waves per SIMD)
+// handed to the register allocator through __launch_bounds__.
+template <bool COUNT, int VARIANT, int MINW>
+__global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
+    __shared__ WaveLds lds[VARIANT >= 1 ? 4 : 1];
     // 16x16 pixel tile per workgroup, 8x8 per wave64.
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -149,170 +559,109 @@ __global__ __launch_bounds__(256) void crt_render_kernel(RenderParams P) {
     const bool valid = x < P.width && y < P.height;
     const int pix = valid ? y * P.width + x : 0;
 
-    Rng s{};
-    V3 pixel = v3(0.f, 0.f, 0.f);
-    int remaining = 0;
+    PathState S;
+    S.s = Rng{0, 0, 0, 0, 0, 0};
+    S.pixel = v3(0.f, 0.f, 0.f);
+    S.o = v3(0, 0, 0); S.d = v3(0, 0, 1); S.thr = v3(1, 1, 1);
+    S.remaining = 0; S.bounce = 0; S.need_new = true; S.rays = 0; S.paths = 0;
     if (valid) {
         const uint32_t* r = P.rng + 6 * (size_t)pix;
-        s.v0 = r[0]; s.v1 = r[1]; s.v2 = r[2]; s.v3 = r[3]; s.v4 = r[4]; s.d = r[5];
-        if (P.accumulate) pixel = v3(P.sum[3 * (size_t)pix], P.sum[3 * (size_t)pix + 1], P.sum[3 * (size_t)pix + 2]);
-        remaining = P.spp;
+        S.s.v0 = r[0]; S.s.v1 = r[1]; S.s.v2 = r[2]; S.s.v3 = r[3]; S.s.v4 = r[4]; S.s.d = r[5];
+        if (P.accumulate) S.pixel = v3(P.sum[3 * (size_t)pix], P.sum[3 * (size_t)pix + 1], P.sum[3 * (size_t)pix + 2]);
+        S.remaining = P.spp;
     }
-    const crt_camera_desc& C = P.cam;
-    const V3 cpos = v3(C.origin[0], C.origin[1], C.origin[2]);
-    const V3 cllc = v3(C.lower_left[0], C.lower_left[1], C.lower_left[2]);
-    const V3 chor = v3(C.horizontal[0], C.horizontal[1], C.horizontal[2]);
-    const V3 cver = v3(C.vertical[0], C.vertical[1], C.vertical[2]);
-    const V3 cright = v3(C.right[0], C.right[1], C.right[2]);
-    const V3 cup = v3(C.up[0], C.up[1], C.up[2]);
-    const float fw = (float)P.width, fh = (float)P.height;
+    const crt_camera_desc& Cd = P.cam;
+    CamRegs C;
+    C.pos = v3(Cd.origin[0], Cd.origin[1], Cd.origin[2]);
+    C.llc = v3(Cd.lower_left[0], Cd.lower_left[1], Cd.lower_left[2]);
+    C.hor = v3(Cd.horizontal[0], Cd.horizontal[1], Cd.horizontal[2]);
+    C.ver = v3(Cd.vertical[0], Cd.vertical[1], Cd.vertical[2]);
+    C.right = v3(Cd.right[0], Cd.right[1], Cd.right[2]);
+    C.up = v3(Cd.up[0], Cd.up[1], Cd.up[2]);
+    C.lens = Cd.lens_radius;
+    C.fw = (float)P.width;
+    C.fh = (float)P.height;
+    TraceCounts cnt{0, 0, 0, 0, 0, 0};
 
-    uint32_t rays = 0, paths = 0;
-    TraceCounts cnt{0, 0, 0};
-    V3 o = v3(0, 0, 0), d = v3(0, 0, 1), thr = v3(1, 1, 1);
-    int bounce = 0;
-    bool need_new = true;
-
-    for (;;) {
-        // ---- phase 1: make sure this lane has a ray to trace (or is done)
-        bool done = false;
+    if (VARIANT == 0) {
         for (;;) {
-            if (need_new) {
-                if (remaining == 0) { done = true; break; }
-                --remaining;
-                // Camera::getRay (Camera.cuh:32-44)
-                float da, db;
-                for (;;) {
-                    da = rand_pm1(s);
-                    db = rand_pm1(s);
-                    if (len2(v3(da, db, 0)) >= 1) continue;
-                    break;
+            if (!next_ray(S, C, x, y, P.max_bounces)) break;
+            ++S.rays;
+            float t;
+            const int hit = trace<COUNT>(P.nodes, P.prims, P.n_nodes, S.o, S.d, t, cnt);
+            shade(S, P, hit, t);
+        }
+    } else if (VARIANT == 2) {
+        // One wave iteration = one traversal step.  A lane whose trace ends parks until at least
+        // `regen_threshold` lanes (or every live lane) are parked; the parked lanes then shade, start
+        // their next ray and rejoin traversal while the others keep stepping.
+        WaveLds& L = lds[wave];
+        const float INF = __builtin_inff();
+        bool live = true, has_result = false;
+        int node = P.n_nodes, hit = -1;
+        float closest = INF;
+        V3 inv = v3(0.f, 0.f, 0.f);
+        L.owner_at[lane] = 0xff;
+        for (;;) {
+            const bool parked = live && node >= P.n_nodes;
+            const int n_parked = __popcll(__ballot(parked));
+            const int n_live = __popcll(__ballot(live));
+            if (n_live == 0) break;
+            if (n_parked >= P.regen_threshold || n_parked == n_live) {
+                if (parked) {
+                    if (has_result) shade(S, P, hit, closest);
+                    live = next_ray(S, C, x, y, P.max_bounces);
+                    has_result = false;
+                    if (live) {
+                        ++S.rays;
+                        has_result = true;
+                        node = 0;
+                        closest = INF;
+                        hit = -1;
+                        inv = v3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
+                        L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
+                        if (COUNT) cnt.trace_calls++;
+                    }
                 }
-                const V3 rd = C.lens_radius * v3(da, db, 0);
-                const V3 off = v3(cright.x * rd.x, cright.y * rd.x, cright.z * rd.x) +
-                               v3(cup.x * rd.y, cup.y * rd.y, cup.z * rd.y);
-                const float u = ((float)x + uniform(s)) / fw;
-                const float v = ((float)y + uniform(s)) / fh;
-                o = cpos + off;
-                d = (((cllc + u * chor) + v * cver) - cpos) - off;
-                thr = v3(1.0f, 1.0f, 1.0f);
-                bounce = 0;
-                need_new = false;
             }
-            // rayColor loop head (CUDAKernels.h:110-121)
-            if (bounce >= P.max_bounces) {            // fell out of the bounce loop: final_color = 0
-                pixel = pixel + v3(0.0f, 0.0f, 0.0f);
-                ++paths;
-                need_new = true;
-                continue;
+            traverse_step<COUNT>(P.nodes, P.prims, P.n_nodes, P.n_prims, P.err, S.o, S.d, inv, node, closest, hit,
+                                 cnt, L, lane);
+        }
+    } else {
+        bool live = true;
+        for (;;) {
+            if (live) live = next_ray(S, C, x, y, P.max_bounces);
+            if (!__ballot(live)) break;
+            float t;
+            const int hit = trace_coop<COUNT>(P.nodes, P.prims, P.n_nodes, P.n_prims, P.err, S.o, S.d, live, t, cnt,
+                                              lds[wave], lane);
+            if (live) {
+                ++S.rays;
+                shade(S, P, hit, t);
             }
-            if (bounce >= 3) {
-                float p = fmaxf(thr.x, fmaxf(thr.y, thr.z));
-                p = fminf(p, 0.95f);
-                if (uniform(s) > p) {
-                    pixel = pixel + v3(0.0f, 0.0f, 0.0f);
-                    ++paths;
-                    need_new = true;
-                    continue;
-                }
-                thr = (1 / p) * thr;
-            }
-            break;
-        }
-        if (done) break;
-
-        // ---- phase 2: closest hit (CUDAKernels.h:123)
-        ++rays;
-        float t;
-        const int hit = trace<COUNT>(P.nodes, P.prims, P.n_nodes, o, d, t, cnt);
-
-        // ---- phase 3: shade
-        if (hit < 0) {                                     // :137-142
-            pixel = pixel + thr * sky(d);
-            ++paths;
-            need_new = true;
-            continue;
-        }
-        const V3 hp = o + t * d;                           // Ray::pointAtDistance
-        V3 outward;
-        uint32_t mat;
-        if (hit >= SPHERE_BIT) {
-            const int p = hit - SPHERE_BIT;
-            const float4 f0 = P.prims[3 * p], f1 = P.prims[3 * p + 1];
-            outward = (1 / f0.w) * (hp - v3(f0.x, f0.y, f0.z));   // Sphere.cuh:44
-            mat = (uint32_t)__float_as_int(f1.y);
-        } else {
-            const float4 f0 = P.prims[3 * hit], f1 = P.prims[3 * hit + 1], f2 = P.prims[3 * hit + 2];
-            outward = unit(cross(v3(f0.w, f1.x, f1.y), v3(f1.z, f1.w, f2.x)));   // Mesh.cuh:303-304
-            mat = (uint32_t)__float_as_int(f2.y);
-        }
-        const bool front = dot(d, outward) < 0;            // HitInfo::setFaceNormal
-        const V3 n = front ? outward : -outward;
-        if (!(mat < (uint32_t)P.n_mats)) {                  // :127 invalid material: same ray again
-            ++bounce;
-            continue;
-        }
-        const float4 m0 = P.mats[3 * mat], m1 = P.mats[3 * mat + 1];
-        const int mtype = __float_as_int(m0.x);
-        if (mtype == CRT_LAMBERTIAN) {                      // Material.cuh:66-77
-            V3 sd = n + rand_unit_vector(s);
-            if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = n;
-            thr = thr * v3(m0.y, m0.z, m0.w);
-            o = hp;
-            d = sd;
-            ++bounce;
-        } else if (mtype == CRT_METAL) {                    // :89-96
-            V3 refl = reflect(d, n);
-            refl = unit(refl) + (m1.w * rand_unit_vector(s));
-            if (dot(refl, n) > 0) {
-                thr = thr * v3(m0.y, m0.z, m0.w);
-                o = hp;
-                d = refl;
-                ++bounce;
-            } else {                                        // absorbed: return Material::emit() = 0
-                pixel = pixel + v3(0.0f, 0.0f, 0.0f);
-                ++paths;
-                need_new = true;
-            }
-        } else if (mtype == CRT_DIELECTRIC) {               // :109-128
-            const float ior = P.mats[3 * mat + 2].x;
-            const float ri = front ? (1.0f / ior) : ior;
-            const V3 ud = unit(d);
-            const double cos_theta = fminf(dot(-ud, n), 1.0f);
-            const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
-            const bool cannot_refract = (double)ri * sin_theta > 1.0;
-            V3 dir;
-            if (cannot_refract || schlick((float)cos_theta, ri) > uniform(s))
-                dir = reflect(ud, n);
-            else
-                dir = refract(ud, n, ri);
-            o = hp;
-            d = dir;
-            ++bounce;   // attenuation (1,1,1): thr unchanged (x*1 == x)
-        } else {                                            // DiffuseLight: return emit() raw
-            const V3 em = (mtype == CRT_DIFFUSE_LIGHT) ? v3(m1.x, m1.y, m1.z) : v3(0.0f, 0.0f, 0.0f);
-            pixel = pixel + em;
-            ++paths;
-            need_new = true;
         }
     }
 
     if (valid) {
         uint32_t* r = P.rng + 6 * (size_t)pix;
-        r[0] = s.v0; r[1] = s.v1; r[2] = s.v2; r[3] = s.v3; r[4] = s.v4; r[5] = s.d;
-        P.sum[3 * (size_t)pix] = pixel.x;
-        P.sum[3 * (size_t)pix + 1] = pixel.y;
-        P.sum[3 * (size_t)pix + 2] = pixel.z;
+        r[0] = S.s.v0; r[1] = S.s.v1; r[2] = S.s.v2; r[3] = S.s.v3; r[4] = S.s.v4; r[5] = S.s.d;
+        P.sum[3 * (size_t)pix] = S.pixel.x;
+        P.sum[3 * (size_t)pix + 1] = S.pixel.y;
+        P.sum[3 * (size_t)pix + 2] = S.pixel.z;
     }
-    const uint64_t wr = wave_sum_u64(rays);
+    const uint64_t wr = wave_sum_u64(S.rays);
     if (COUNT) {
         const uint64_t wb = wave_sum_u64(cnt.boxes), wt = wave_sum_u64(cnt.tris);
-        const uint64_t ws = wave_sum_u64(cnt.spheres), wp = wave_sum_u64(paths);
+        const uint64_t ws = wave_sum_u64(cnt.spheres), wp = wave_sum_u64(S.paths);
         if (lane == 0) {
             atomicAdd(&P.counters[1], (unsigned long long)wb);
             atomicAdd(&P.counters[2], (unsigned long long)wt);
             atomicAdd(&P.counters[3], (unsigned long long)ws);
             atomicAdd(&P.counters[4], (unsigned long long)wp);
+            // scheduling diagnostics (variant 1): lane-slots offered by traversal steps / leaf rounds,
+            // and wave-level trace calls (all uniform per wave)
+            atomicAdd(&P.counters[5], 64ull * cnt.step_slots);
+            atomicAdd(&P.counters[6], 64ull * cnt.round_slots + ((unsigned long long)cnt.trace_calls << 40));
         }
     }
     if (lane == 0) atomicAdd(&P.counters[0], (unsigned long long)wr);
@@ -379,6 +728,16 @@ __global__ void crt_selftest_math_kernel(const float* a, const float* b, int n, 
     out[4 * i + 3] = (float)sqrt((double)fabsf(x));
     out64[2 * i] = sqrt(dx);
     out64[2 * i + 1] = 1.0 - dx * dx;
+}
+
+__global__ __launch_bounds__(64) void crt_selftest_scan_kernel(const int* in, int* out, int n_waves) {
+    const int w = blockIdx.x;
+    if (w >= n_waves) return;
+    const int lane = threadIdx.x;
+    const int x = in[64 * w + lane];
+    out[3 * (64 * w + lane)] = wave_inclusive_scan(x, lane);
+    out[3 * (64 * w + lane) + 1] = wave_inclusive_scan_shfl(x, lane);
+    out[3 * (64 * w + lane) + 2] = wave_inclusive_max_scan(x, lane);
 }
 
 __global__ void crt_selftest_rng_kernel(const uint32_t* st_in, int n, int n_draw, float* out) {
@@ -558,6 +917,10 @@ struct crt_renderer {
     bool has_camera = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    int variant = 2;               // see crt_renderer_set_kernel_variant
+    unsigned long long diag[3] = {0, 0, 0};
+    int regen_threshold = 24;
+    int min_waves = 5;             // variant 2 occupancy target: 1 (compiler's choice), 5, 6 or 8
 };
 
 namespace {
@@ -707,6 +1070,24 @@ int crt_renderer_init_rand(crt_renderer* R, unsigned long long seed, unsigned lo
     return CRT_OK;
 }
 
+int crt_renderer_set_kernel_variant(crt_renderer* R, int variant) {
+    if (!R || variant < 0 || variant > 2) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant");
+    R->variant = variant;
+    return CRT_OK;
+}
+
+int crt_renderer_set_occupancy_target(crt_renderer* R, int waves_per_simd) {
+    if (!R || waves_per_simd < 1 || waves_per_simd > 8) return set_error(CRT_ERR_INVALID_ARGUMENT, "waves per SIMD 1..8");
+    R->min_waves = waves_per_simd;
+    return CRT_OK;
+}
+
+int crt_renderer_set_regen_threshold(crt_renderer* R, int lanes) {
+    if (!R || lanes < 1 || lanes > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "threshold must be 1..64");
+    R->regen_threshold = lanes;
+    return CRT_OK;
+}
+
 int crt_renderer_set_camera(crt_renderer* R, const crt_camera_desc* cam) {
     if (!R || !cam) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
     R->cam = *cam;
@@ -724,16 +1105,27 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     HIP_TRY(hipMemsetAsync(R->d_counters, 0, 8 * sizeof(unsigned long long), st));
     RenderParams P;
     P.nodes = S->d_nodes; P.prims = S->d_prims; P.mats = S->d_mats;
-    P.n_nodes = S->n_nodes; P.n_mats = S->n_mats;
+    P.n_nodes = S->n_nodes; P.n_mats = S->n_mats; P.n_prims = S->n_prims;
+    P.err = reinterpret_cast<unsigned*>(R->d_counters + 7);
     P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
     P.accumulate = (flags & CRT_RENDER_ACCUMULATE) ? 1 : 0;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     dim3 grid((R->width + 15) / 16, (R->height + 15) / 16), block(256);
     HIP_TRY(hipEventRecord(R->ev0, st));
-    if (flags & CRT_RENDER_COUNT_WORK)
-        hipLaunchKernelGGL(crt_render_kernel<true>, grid, block, 0, st, P);
-    else
-        hipLaunchKernelGGL(crt_render_kernel<false>, grid, block, 0, st, P);
+    const bool cnt = (flags & CRT_RENDER_COUNT_WORK) != 0;
+    P.regen_threshold = R->regen_threshold;
+#define CRT_LAUNCH(V, W)                                                                     \
+    do {                                                                                     \
+        if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, V, W>), grid, block, 0, st, P);  \
+        else hipLaunchKernelGGL((crt_render_kernel<false, V, W>), grid, block, 0, st, P);     \
+    } while (0)
+    if (R->variant == 0) CRT_LAUNCH(0, 1);
+    else if (R->variant == 1) CRT_LAUNCH(1, 1);
+    else if (R->min_waves >= 8) CRT_LAUNCH(2, 8);
+    else if (R->min_waves >= 6) CRT_LAUNCH(2, 6);
+    else if (R->min_waves >= 5) CRT_LAUNCH(2, 5);
+    else CRT_LAUNCH(2, 1);
+#undef CRT_LAUNCH
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(R->ev1, st));
     R->timed = true;
@@ -791,9 +1183,17 @@ int crt_renderer_get_counters(crt_renderer* R, crt_work_counters* out) {
     if (!R || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
     unsigned long long c[8];
     if (int rc = read_dev(R, c, R->d_counters, sizeof c)) return rc;
+    R->diag[0] = c[5]; R->diag[1] = c[6] & ((1ull << 40) - 1); R->diag[2] = c[6] >> 40;
     out->rays = c[0]; out->box_tests = c[1]; out->tri_tests = c[2]; out->sphere_tests = c[3]; out->paths = c[4];
+    if (c[7]) return set_error(CRT_ERR_HIP, "render kernel reported an internal indexing error");
     return CRT_OK;
 }
+int crt_renderer_get_schedule_stats(crt_renderer* R, unsigned long long* out3) {
+    if (!R || !out3) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    out3[0] = R->diag[0]; out3[1] = R->diag[1]; out3[2] = R->diag[2];
+    return CRT_OK;
+}
+
 float* crt_renderer_linear_device_ptr(crt_renderer* R) { return R ? R->d_sum : nullptr; }
 uint8_t* crt_renderer_rgba_device_ptr(crt_renderer* R) { return R ? R->d_rgba : nullptr; }
 uint32_t* crt_renderer_rng_device_ptr(crt_renderer* R) { return R ? R->d_rng : nullptr; }
@@ -822,6 +1222,21 @@ int crt_selftest_math(const float* a, const float* b, int n, float* out, double*
     HIP_TRY(hipMemcpy(out, dout, n * 16, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(out64, d64, n * 16, hipMemcpyDeviceToHost));
     (void)hipFree(da); (void)hipFree(db); (void)hipFree(dout); (void)hipFree(d64);
+    return CRT_OK;
+}
+
+int crt_selftest_scan(const int* in, int n_waves, int* out) {
+    if (!in || !out || n_waves <= 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    if (int rc = use_device(0)) return rc;
+    int *din, *dout;
+    HIP_TRY(hipMalloc((void**)&din, (size_t)n_waves * 64 * 4));
+    HIP_TRY(hipMalloc((void**)&dout, (size_t)n_waves * 64 * 12));
+    HIP_TRY(hipMemcpy(din, in, (size_t)n_waves * 64 * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(crt_selftest_scan_kernel, dim3(n_waves), dim3(64), 0, 0, din, dout, n_waves);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(out, dout, (size_t)n_waves * 64 * 12, hipMemcpyDeviceToHost));
+    (void)hipFree(din);
+    (void)hipFree(dout);
     return CRT_OK;
 }
 

@@ -15,8 +15,12 @@ pytestmark = pytest.mark.gpu
 RMS_TOL = 1e-4
 
 
-def _render(dev_scene, w, h, spp, bounces, seed=41, subseq=0, cam=None):
+VARIANTS = [0, 1, 2]
+
+
+def _render(dev_scene, w, h, spp, bounces, seed=41, subseq=0, cam=None, variant=2):
     r = crt_amd.Renderer(w, h)
+    r.set_kernel_variant(variant)
     r.set_camera(cam or crt_amd.camera(spp))
     r.init_rand(seed, subseq)
     r.render(dev_scene, spp, bounces)
@@ -52,6 +56,21 @@ def test_selftest_math_ieee():
     assert np.array_equal(out64.view(np.uint64), exp64.view(np.uint64))
 
 
+def test_wave_scans():
+    import ctypes as C
+    from crt_amd import _lib
+    rng = np.random.default_rng(1)
+    n = 64
+    x = rng.integers(-1, 50, size=(n, 64)).astype(np.int32)
+    x[0] = 0
+    x[1] = -1
+    out = np.zeros((n, 64, 3), np.int32)
+    crt_amd.check(_lib.hip().crt_selftest_scan(x.ctypes.data_as(C.c_void_p), n, out.ctypes.data_as(C.c_void_p)))
+    assert np.array_equal(out[..., 0], np.cumsum(x, axis=1))
+    assert np.array_equal(out[..., 1], np.cumsum(x, axis=1))
+    assert np.array_equal(out[..., 2], np.maximum.accumulate(x, axis=1))
+
+
 def test_rng_matches_oracle():
     import ctypes as C
     from crt_amd import _lib
@@ -68,28 +87,31 @@ def test_rng_matches_oracle():
         assert np.array_equal(u[i].view(np.uint32), of.view(np.uint32))
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("bounces", [4, 20])
-def test_config_a_full_frame(device_scenes, oracle_scenes, bounces):
+def test_config_a_full_frame(device_scenes, oracle_scenes, bounces, variant):
     """Config A: Cornell (no bunny) 256x256, 16 spp — whole frame bit-exact vs oracle."""
     w = h = 256
     spp = 16
     _, dev = device_scenes["cornell"]
     cam = crt_amd.camera(spp)
-    r = _render(dev, w, h, spp, bounces, cam=cam)
+    r = _render(dev, w, h, spp, bounces, cam=cam, variant=variant)
     o_sum, o_rgba, o_cnt = oracle_scenes["cornell"].render(crt_amd.camera_floats(cam), w, h, spp, bounces)
     _assert_parity(r.linear(), r.rgba8(), o_sum, o_rgba, spp)
     assert r.counters()["rays"] == o_cnt["rays"] == {4: 3197876, 20: 3420058}[bounces]
 
 
-def test_cornell_bunny_crop_parity(device_scenes, oracle_scenes):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_cornell_bunny_crop_parity(device_scenes, oracle_scenes, variant):
     """Cornell + bunny proxy (glass), 128x72 frame, 32 spp, 20 bounces."""
     w, h, spp = 128, 72, 32
     _, dev = device_scenes["cornell_bunny"]
     cam = crt_amd.camera(spp)
-    r = _render(dev, w, h, spp, 20, cam=cam)
+    r = _render(dev, w, h, spp, 20, cam=cam, variant=variant)
     o_sum, o_rgba, o_cnt = oracle_scenes["cornell_bunny"].render(crt_amd.camera_floats(cam), w, h, spp, 20)
     _assert_parity(r.linear(), r.rgba8(), o_sum, o_rgba, spp)
     r2 = crt_amd.Renderer(w, h)
+    r2.set_kernel_variant(variant)
     r2.set_camera(cam)
     r2.init_rand(41)
     r2.render(dev, spp, 20, count_work=True)
@@ -115,13 +137,14 @@ def test_chunked_accumulate_equals_single(device_scenes):
     assert np.array_equal(a.rng_state(), b.rng_state())
 
 
-def test_full_size_frame_sampled_pixels(device_scenes, oracle_scenes):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_full_size_frame_sampled_pixels(device_scenes, oracle_scenes, variant):
     """Headline geometry (2560x1440) at reduced spp; a band of pixels checked against the oracle,
     plus size-independent properties (determinism, ray count = counting-kernel count)."""
     w, h, spp = 2560, 1440, 4
     _, dev = device_scenes["cornell_bunny"]
     cam = crt_amd.camera(spp)
-    r = _render(dev, w, h, spp, 20, cam=cam)
+    r = _render(dev, w, h, spp, 20, cam=cam, variant=variant)
     lin = r.linear()
     rays = r.counters()["rays"]
     r.init_rand(41)
@@ -130,9 +153,10 @@ def test_full_size_frame_sampled_pixels(device_scenes, oracle_scenes):
     assert np.array_equal(lin.view(np.uint32), r.linear().view(np.uint32)), "not deterministic"
     assert r.counters()["rays"] == rays
     cf = crt_amd.camera_floats(cam)
+    rgba = r.rgba8()
     for (x0, y0, x1, y1) in [(0, 0, 64, 4), (1200, 700, 1296, 708), (2496, 1436, 2560, 1440), (1700, 900, 1760, 960)]:
         o_sum, o_rgba, _ = oracle_scenes["cornell_bunny"].render(cf, w, h, spp, 20, rect=(x0, y0, x1, y1))
-        _assert_parity(lin[y0:y1, x0:x1], r.rgba8()[y0:y1, x0:x1], o_sum, o_rgba, spp)
+        _assert_parity(lin[y0:y1, x0:x1], rgba[y0:y1, x0:x1], o_sum, o_rgba, spp)
 
 
 def test_sharded_n1_is_reference_frame_and_shards_sum(device_scenes):
