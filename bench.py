@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="target CPU-baseline sample duration")
     ap.add_argument("--save-ppm", default="", help="rank 0 writes the resolved frame here")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--kernel-variant", type=int, default=None, help="render-kernel variant (default: library's)")
     return ap.parse_args()
 
 
@@ -113,9 +115,13 @@ def main():
     rank, local, world = dist_env()
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    local = local % max(1, torch.cuda.device_count())   # rehearsal: several ranks may share one GPU (gloo)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(args.dist_backend)
     log_r = log if rank == 0 else (lambda *a: None)
 
     def barrier():
@@ -151,6 +157,8 @@ def main():
 
     cam = crt_amd.camera(args.spp)
     r = crt_amd.Renderer(W, H, local)
+    if args.kernel_variant is not None:
+        r.set_kernel_variant(args.kernel_variant)
     r.set_camera(cam)
     fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world)
     log_r(f"[plan] {world} rank(s), spp per rank {[fr.spp] if world == 1 else 'spp/N'}")
@@ -233,7 +241,9 @@ def main():
                        if args.scene == "cornell_bunny" else f"{args.scene} {W}x{H} {args.spp}spp {args.bounces} bounces",
                        "width": W, "height": H, "spp": args.spp, "max_bounces": args.bounces, "seed": args.seed,
                        "triangles": counts["n_indices"] // 3,
-                       "parallelism": f"spp-shard x{world}" + (" + RCCL reduce of fp32 framebuffer" if world > 1 else "")},
+                       "parallelism": f"spp-shard x{world}" + ((" + RCCL reduce of fp32 framebuffer" if args.dist_backend == "nccl"
+                                                                  else f" + {args.dist_backend} reduce (rehearsal)")
+                                                                 if world > 1 else "")},
             "frame_wall_s": round(ms_per_step / 1e3, 4),
             "rays_per_frame": rays_frame,
             "paths_per_s": round(W * H * args.spp * args.steps / elapsed, 1),

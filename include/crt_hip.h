@@ -162,10 +162,10 @@ void crt_renderer_destroy(crt_renderer* r);
  * subsequence_base = shard * width * height for spp sharding. */
 int  crt_renderer_init_rand(crt_renderer* r, unsigned long long seed, unsigned long long subsequence_base, void* stream);
 int  crt_renderer_set_camera(crt_renderer* r, const crt_camera_desc* cam);
-/* Render-kernel variant (identical results, different wave scheduling): 0 = per-lane BVH traversal
- * with per-lane leaf loops; 1 = per-lane traversal with wave-cooperative leaf intersection;
+/* Render-kernel variant (identical results, different wave scheduling; default 3): 0 = per-lane BVH
+ * traversal with per-lane leaf loops; 1 = per-lane traversal with wave-cooperative leaf intersection;
  * 2 = 1 + traversal-step scheduling with parked-lane regeneration (lanes start their next ray
- * without waiting for the wave's slowest trace). */
+ * without waiting for the wave's slowest trace); 3 = 2 + next-node prefetch overlapping the leaf rounds. */
 int  crt_renderer_set_kernel_variant(crt_renderer* r, int variant);
 /* Variant 2: number of parked lanes (1..64, default 32) that triggers a shading/regeneration pass. */
 int  crt_renderer_set_regen_threshold(crt_renderer* r, int lanes);
@@ -201,6 +201,9 @@ float crt_renderer_last_kernel_ms(crt_renderer* r);
 /* For n inputs a[i], b[i] (f32) computes on the device: a/b, sqrtf(|a|), 1/a, (double)sqrt((double)|a|)
  * into out[4*i..4*i+3] (the last one converted to float bits as a double->float cast). */
 int crt_selftest_math(const float* a, const float* b, int n, float* out, double* out_f64);
+/* Exhaustive reciprocal self-test: counts floats x with bit patterns in [lo_bits, hi_bits) (and -x) for which
+ * the kernel's fast reciprocal (v_rcp_f32 + FMA Newton step) differs from IEEE 1.f/x; first_bad = lowest such. */
+int crt_selftest_rcp(uint32_t lo_bits, uint32_t hi_bits, unsigned long long* mismatches, uint32_t* first_bad);
 /* Wave64 scan self-test: for n_waves x 64 ints, out[3*i..] = DPP inclusive sum, ds_bpermute inclusive sum,
  * DPP inclusive max (per wave of 64 consecutive entries). */
 int crt_selftest_scan(const int* in, int n_waves, int* out);

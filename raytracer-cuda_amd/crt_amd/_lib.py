@@ -72,7 +72,7 @@ HIP_SYMBOLS = [
     "crt_renderer_rgba_device_ptr", "crt_renderer_rng_device_ptr", "crt_renderer_last_kernel_ms",
     "crt_renderer_attach_linear", "crt_renderer_set_kernel_variant", "crt_renderer_get_schedule_stats",
     "crt_renderer_set_regen_threshold", "crt_renderer_set_occupancy_target",
-    "crt_selftest_math", "crt_selftest_rng", "crt_selftest_scan",
+    "crt_selftest_math", "crt_selftest_rng", "crt_selftest_scan", "crt_selftest_rcp",
 ]
 HOST_SYMBOLS = [
     "crth_scene_load", "crth_scene_destroy", "crth_scene_desc", "crth_scene_upload", "crth_scene_counts",
@@ -129,6 +129,7 @@ def hip():
             "crt_selftest_math": ([P, P, i32, P, P], i32),
             "crt_selftest_rng": ([u64, P, i32, i32, P, P], i32),
             "crt_selftest_scan": ([P, i32, P], i32),
+            "crt_selftest_rcp": ([C.c_uint32, C.c_uint32, P, P], i32),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)

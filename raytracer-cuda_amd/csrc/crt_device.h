@@ -56,6 +56,20 @@ __device__ __forceinline__ V3 refract(V3 uv, V3 n, float eta) {                 
     return perp + par;
 }
 
+// Correctly rounded 1/x for the Möller–Trumbore determinant: v_rcp_f32 + one FMA Newton step.
+// Exhaustively verified on gfx950 against IEEE division for EVERY float with
+// 1e-8 <= |x| < RCP_FAST_MAX (crt_selftest_rcp, tests/test_gpu_parity.py); outside that range
+// the exact division sequence is used, so the result always equals 1.f / x bit for bit.
+constexpr float RCP_FAST_MAX = 8.507059e37f;   // 2^126: reciprocal stays a normal float
+__device__ __forceinline__ float rcp_newton(float x) {
+    const float r = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+}
+__device__ __forceinline__ float recip_exact(float x) {
+    return fabsf(x) < RCP_FAST_MAX ? rcp_newton(x) : 1.0f / x;
+}
+
 // ------------------------------------------------------------------ XORWOW
 // cuRAND XORWOW (CUDA 12.5 curand_kernel.h: curand, _curand_uniform) — see DESIGN.md.
 struct Rng { uint32_t v0, v1, v2, v3, v4, d; };

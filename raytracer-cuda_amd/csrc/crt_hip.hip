@@ -199,7 +199,7 @@ __device__ __forceinline__ float tri_test(const float4* __restrict__ prims, int 
     const V3 h = cross(d, e2);
     const float det = dot(e1, h);
     if (fabsf(det) < 1e-8f) return -1.f;
-    const float f = 1.f / det;
+    const float f = recip_exact(det);          // == 1.f / det bit for bit (see crt_device.h)
     const V3 s = o - v3(f0.x, f0.y, f0.z);
     const float u = f * dot(s, h);
     if (u < 0.f || u > 1.f) return -1.f;
@@ -332,17 +332,19 @@ __device__ int trace_coop(const float4* __restrict__ nodes, const float4* __rest
 
 // One wave traversal step (variant 2): every lane with node < n_nodes tests one node; the leaves
 // reached in this step are intersected cooperatively (same rounds as trace_coop).  All 64 lanes call it.
-template <bool COUNT>
+// PREFETCH: the caller keeps the current node's 32 B in (pA, pB); the next node is loaded right after
+// the box test so its latency overlaps this step's leaf rounds.
+template <bool COUNT, bool PREFETCH>
 __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                                               int n_nodes, int n_prims, unsigned* err, V3 o, V3 d, V3 inv,
                                               int& node, float& closest, int& hit, TraceCounts& cnt, WaveLds& L,
-                                              int lane) {
+                                              int lane, float4& pA, float4& pB) {
     const float INF = __builtin_inff();
     if (COUNT) cnt.step_slots++;
     int leaf_n = 0, leaf_first = 0;
     if (node < n_nodes) {
-        const float4 A = nodes[2 * node];
-        const float4 B = nodes[2 * node + 1];
+        const float4 A = PREFETCH ? pA : nodes[2 * node];
+        const float4 B = PREFETCH ? pB : nodes[2 * node + 1];
         const int a = __float_as_int(B.z);
         const int b = __float_as_int(B.w);
         const bool scene_level = (b == NODE_SCENE_INNER) || (b >= SPHERE_BIT);
@@ -368,6 +370,10 @@ __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, 
             }
         }
         node = next;
+        if (PREFETCH && next < n_nodes) {
+            pA = nodes[2 * next];
+            pB = nodes[2 * next + 1];
+        }
     }
     if (!__ballot(leaf_n > 0)) return;
     const int incl = wave_inclusive_scan(leaf_n, lane);
@@ -591,7 +597,9 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
             const int hit = trace<COUNT>(P.nodes, P.prims, P.n_nodes, S.o, S.d, t, cnt);
             shade(S, P, hit, t);
         }
-    } else if (VARIANT == 2) {
+    } else if (VARIANT == 2 || VARIANT == 3) {
+        constexpr bool PF = VARIANT == 3;
+        float4 pA = make_float4(0.f, 0.f, 0.f, 0.f), pB = pA;
         // One wave iteration = one traversal step.  A lane whose trace ends parks until at least
         // `regen_threshold` lanes (or every live lane) are parked; the parked lanes then shade, start
         // their next ray and rejoin traversal while the others keep stepping.
@@ -620,12 +628,16 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
                         hit = -1;
                         inv = v3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
                         L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
+                        if (PF) {
+                            pA = P.nodes[0];
+                            pB = P.nodes[1];
+                        }
                         if (COUNT) cnt.trace_calls++;
                     }
                 }
             }
-            traverse_step<COUNT>(P.nodes, P.prims, P.n_nodes, P.n_prims, P.err, S.o, S.d, inv, node, closest, hit,
-                                 cnt, L, lane);
+            traverse_step<COUNT, PF>(P.nodes, P.prims, P.n_nodes, P.n_prims, P.err, S.o, S.d, inv, node, closest,
+                                     hit, cnt, L, lane, pA, pB);
         }
     } else {
         bool live = true;
@@ -728,6 +740,25 @@ __global__ void crt_selftest_math_kernel(const float* a, const float* b, int n, 
     out[4 * i + 3] = (float)sqrt((double)fabsf(x));
     out64[2 * i] = sqrt(dx);
     out64[2 * i + 1] = 1.0 - dx * dx;
+}
+
+// Exhaustive check of rcp_newton against IEEE 1.f/x over bit patterns [lo, hi) of positive floats
+// (the negative half is the mirror image: both rcp and the FMAs are sign-symmetric, still checked).
+__global__ __launch_bounds__(256) void crt_selftest_rcp_kernel(uint32_t lo, uint32_t hi, unsigned long long* bad,
+                                                               uint32_t* first_bad) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    unsigned long long nbad = 0;
+    for (uint32_t b = lo + blockIdx.x * blockDim.x + threadIdx.x; b < hi && b >= lo; b += stride) {
+        const float x = __uint_as_float(b);
+        const float a = rcp_newton(x), c = 1.0f / x;
+        const float an = rcp_newton(-x), cn = 1.0f / -x;
+        if (__float_as_uint(a) != __float_as_uint(c) || __float_as_uint(an) != __float_as_uint(cn)) {
+            ++nbad;
+            atomicMin(first_bad, b);
+        }
+        if (b > 0xffffffffu - stride) break;
+    }
+    if (nbad) atomicAdd(bad, nbad);
 }
 
 __global__ __launch_bounds__(64) void crt_selftest_scan_kernel(const int* in, int* out, int n_waves) {
@@ -917,7 +948,7 @@ struct crt_renderer {
     bool has_camera = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
-    int variant = 2;               // see crt_renderer_set_kernel_variant
+    int variant = 3;               // see crt_renderer_set_kernel_variant
     unsigned long long diag[3] = {0, 0, 0};
     int regen_threshold = 24;
     int min_waves = 5;             // variant 2 occupancy target: 1 (compiler's choice), 5, 6 or 8
@@ -1071,7 +1102,7 @@ int crt_renderer_init_rand(crt_renderer* R, unsigned long long seed, unsigned lo
 }
 
 int crt_renderer_set_kernel_variant(crt_renderer* R, int variant) {
-    if (!R || variant < 0 || variant > 2) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant");
+    if (!R || variant < 0 || variant > 3) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant");
     R->variant = variant;
     return CRT_OK;
 }
@@ -1121,6 +1152,11 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     } while (0)
     if (R->variant == 0) CRT_LAUNCH(0, 1);
     else if (R->variant == 1) CRT_LAUNCH(1, 1);
+    else if (R->variant == 3) {
+        if (R->min_waves >= 5) CRT_LAUNCH(3, 5);
+        else if (R->min_waves >= 4) CRT_LAUNCH(3, 4);
+        else CRT_LAUNCH(3, 1);
+    }
     else if (R->min_waves >= 8) CRT_LAUNCH(2, 8);
     else if (R->min_waves >= 6) CRT_LAUNCH(2, 6);
     else if (R->min_waves >= 5) CRT_LAUNCH(2, 5);
@@ -1222,6 +1258,24 @@ int crt_selftest_math(const float* a, const float* b, int n, float* out, double*
     HIP_TRY(hipMemcpy(out, dout, n * 16, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(out64, d64, n * 16, hipMemcpyDeviceToHost));
     (void)hipFree(da); (void)hipFree(db); (void)hipFree(dout); (void)hipFree(d64);
+    return CRT_OK;
+}
+
+int crt_selftest_rcp(uint32_t lo_bits, uint32_t hi_bits, unsigned long long* mismatches, uint32_t* first_bad) {
+    if (!mismatches || !first_bad) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    if (int rc = use_device(0)) return rc;
+    unsigned long long* dbad;
+    uint32_t* dfirst;
+    HIP_TRY(hipMalloc((void**)&dbad, 8));
+    HIP_TRY(hipMalloc((void**)&dfirst, 4));
+    HIP_TRY(hipMemset(dbad, 0, 8));
+    HIP_TRY(hipMemset(dfirst, 0xff, 4));
+    hipLaunchKernelGGL(crt_selftest_rcp_kernel, dim3(8192), dim3(256), 0, 0, lo_bits, hi_bits, dbad, dfirst);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(mismatches, dbad, 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(first_bad, dfirst, 4, hipMemcpyDeviceToHost));
+    (void)hipFree(dbad);
+    (void)hipFree(dfirst);
     return CRT_OK;
 }
 

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 RMS_TOL = 1e-4
 
 
-VARIANTS = [0, 1, 2]
+VARIANTS = [0, 1, 2, 3]
 
 
 def _render(dev_scene, w, h, spp, bounces, seed=41, subseq=0, cam=None, variant=2):
@@ -54,6 +54,18 @@ def test_selftest_math_ieee():
         exp64 = np.stack([np.sqrt(dx), 1.0 - dx * dx], axis=1)
     assert np.array_equal(out.view(np.uint32), exp.view(np.uint32))
     assert np.array_equal(out64.view(np.uint64), exp64.view(np.uint64))
+
+
+def test_fast_reciprocal_exhaustive():
+    """rcp_newton(x) == IEEE 1.f/x for EVERY float with 1e-8 <= |x| < 2^126 (both signs); the kernel uses
+    it only in that range (crt_device.h::recip_exact), so the MT determinant reciprocal stays exact."""
+    import ctypes as C
+    from crt_amd import _lib
+    lo = int(np.float32(1e-8).view(np.uint32))
+    hi = int(np.float32(8.507059e37).view(np.uint32))
+    bad, first = C.c_ulonglong(0), C.c_uint32(0)
+    crt_amd.check(_lib.hip().crt_selftest_rcp(lo, hi, C.byref(bad), C.byref(first)))
+    assert bad.value == 0, f"{bad.value} mismatches, first bits {first.value:#010x}"
 
 
 def test_wave_scans():

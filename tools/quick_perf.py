@@ -28,8 +28,8 @@ print("scene", a.scene, "load+build+upload %.2fs" % (time.time() - t), sc.stats(
 r = crt_amd.Renderer(a.w, a.h)
 r.set_camera(crt_amd.camera(a.spp))
 variants = [(int(v), int(th), int(oc)) for v in a.variants.split(",")
-            for th in (a.thresholds.split(",") if v == "2" else ["32"])
-            for oc in (a.occupancy.split(",") if v == "2" else ["1"])]
+            for th in (a.thresholds.split(",") if v in ("2", "3") else ["32"])
+            for oc in (a.occupancy.split(",") if v in ("2", "3") else ["1"])]
 for i in range(a.reps):
     for var, th, oc in variants:          # interleaved A/B in one process
         r.set_kernel_variant(var)
