@@ -8,6 +8,12 @@ from fresh per-pixel RNG state: initRandState-equivalent + the render kernel +
 triangles, materials) is resident in HBM before the timed region.  N GPUs shard the
 frame's samples (strong scaling: total work per frame is fixed).
 
+--bvh rebuilt (default) traverses the CRT_BVH_REBUILT 4-wide SAH BVH (same hit rule as the
+reference); at N=1 the same frame is then also rendered through the reference's own BVH and the
+image parity (per-channel RMS of the resolved colour, north-star bar 1e-4; bit-identical pixel
+fraction) is reported in the JSON line together with that frame's kernel time.  --bvh reference
+times the bit-exact reference-BVH path itself.
+
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
@@ -56,6 +62,11 @@ def parse():
     ap.add_argument("--save-ppm", default="", help="rank 0 writes the resolved frame here")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--kernel-variant", type=int, default=None, help="render-kernel variant (default: library's)")
+    ap.add_argument("--bvh", default="rebuilt", choices=["rebuilt", "reference"])
+    ap.add_argument("--bvh-width", type=int, default=4, help="rebuilt BVH: 4 (variant 4) or 2 (threaded)")
+    ap.add_argument("--leaf-size", type=int, default=4)
+    ap.add_argument("--traversal-cost", type=float, default=3.0)
+    ap.add_argument("--no-parity", action="store_true", help="skip the reference-BVH parity frame")
     return ap.parse_args()
 
 
@@ -148,7 +159,13 @@ def main():
     files = assets.scene_files(args.scene)
     t = time.perf_counter()
     hs = crt_amd.HostScene(files)
-    scene = hs.upload(local)
+    ref_scene = hs.upload(local)
+    scene = ref_scene
+    bvh_desc = "reference (bit-exact)"
+    if args.bvh == "rebuilt":
+        scene = hs.upload(local, bvh="rebuilt", width=args.bvh_width, leaf_size=args.leaf_size,
+                          traversal_cost=args.traversal_cost)
+        bvh_desc = (f"rebuilt {args.bvh_width}-wide SAH, leaf<={args.leaf_size}, C_trav={args.traversal_cost:g}")
     t_scene = time.perf_counter() - t
     st = scene.stats()
     counts = hs.counts()
@@ -202,16 +219,20 @@ def main():
         r.synchronize()
         work = r.counters()
         assert work["rays"] == rays_rank, "counting kernel disagrees with the timed kernel"
+    variant = 4 if st.get("width") == 4 else (args.kernel_variant if args.kernel_variant is not None else 3)
+    kname = f"crt_render_kernel<false, {variant}, 5>"
+    if work is not None:
         bytes_launch = (B_BOX * work["box_tests"] + B_TRI * work["tri_tests"] + B_SPHERE * work["sphere_tests"]
                         + B_RAY * work["rays"] + B_PIXEL * W * H)
         flops_launch = (F_BOX * work["box_tests"] + F_TRI * work["tri_tests"] + F_SPHERE * work["sphere_tests"]
                         + F_RAY * work["rays"])
         achieved = bytes_launch / (kernel_ms_avg / 1e3) / 1e9
-        wkey = f"{args.scene}_{W}x{H}_{fr.spp}spp_{args.bounces}b"
+        wkey = f"{args.scene}_{W}x{H}_{fr.spp}spp_{args.bounces}b" + ("" if args.bvh == "reference" else
+                                                                      f"_rebuilt{args.bvh_width}")
         traffic, tsrc = pmc_traffic(wkey)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "bytes_per_launch": int(bytes_launch), "kernel": "crt_render_kernel<false>",
+                    "bytes_per_launch": int(bytes_launch), "kernel": kname,
                     "kernel_ms_avg": round(kernel_ms_avg, 3),
                     "per_ray": {"box_tests": round(work["box_tests"] / work["rays"], 3),
                                 "tri_tests": round(work["tri_tests"] / work["rays"], 3),
@@ -223,6 +244,36 @@ def main():
         valu = flops_launch / (kernel_ms_avg / 1e3) / 1e12
         roofline_valu = {"bound": "valu", "achieved": round(valu, 2), "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
                          "frac": round(valu / VALU_PEAK_TOPS, 4), "ops_per_launch": int(flops_launch)}
+
+    # parity of the timed configuration against the reference's own BVH on the same frame (N=1)
+    parity = None
+    if world == 1 and args.bvh == "rebuilt" and not args.no_parity:
+        import numpy as np
+        r.init_rand(args.seed, fr.subseq)
+        r.render(scene, fr.spp, args.bounces)
+        r.synchronize()
+        lin = r.linear()
+        r.init_rand(args.seed, fr.subseq)
+        r.render(ref_scene, fr.spp, args.bounces)
+        r.synchronize()
+        ref_ms = r.last_kernel_ms()
+        ref_rays = r.counters()["rays"]
+        lin_ref = r.linear()
+        scale = crt_amd.pixel_sample_scale(args.spp)
+        d = ((lin - lin_ref) * scale).astype(np.float64).reshape(-1, 3)
+        rms = [float(v) for v in np.sqrt(np.mean(d * d, axis=0))]
+        eq = float(np.mean(np.all(lin.view(np.uint32) == lin_ref.view(np.uint32), axis=-1)))
+        parity = {"against": "same frame through the reference's own BVH (bit-exact path, == oracle)",
+                  "rms_per_channel": [round(v, 8) for v in rms], "tolerance": 1e-4,
+                  "pass": bool(max(rms) <= 1e-4), "pixels_bit_identical": round(eq, 7),
+                  "reference_bvh_kernel_ms": round(ref_ms, 3),
+                  "reference_bvh_mrays_s": round(ref_rays / ref_ms / 1e3, 1), "rays_rel_diff": (rays_rank - ref_rays) / ref_rays}
+        log_r(f"[parity] vs reference BVH: RMS {rms}, {eq:.6f} of pixels bit-identical; reference BVH kernel "
+              f"{ref_ms:.1f} ms")
+        r.init_rand(args.seed, fr.subseq)   # leave the timed frame in the framebuffer
+        r.render(scene, fr.spp, args.bounces)
+        r.resolve(scale)
+        r.synchronize()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -240,7 +291,7 @@ def main():
             "config": {"workload": f"{args.scene} {W}x{H} {args.spp}spp {args.bounces} bounces (configs[2])"
                        if args.scene == "cornell_bunny" else f"{args.scene} {W}x{H} {args.spp}spp {args.bounces} bounces",
                        "width": W, "height": H, "spp": args.spp, "max_bounces": args.bounces, "seed": args.seed,
-                       "triangles": counts["n_indices"] // 3,
+                       "triangles": counts["n_indices"] // 3, "bvh": bvh_desc, "kernel_variant": variant,
                        "parallelism": f"spp-shard x{world}" + ((" + RCCL reduce of fp32 framebuffer" if args.dist_backend == "nccl"
                                                                   else f" + {args.dist_backend} reduce (rehearsal)")
                                                                  if world > 1 else "")},
@@ -248,7 +299,7 @@ def main():
             "rays_per_frame": rays_frame,
             "paths_per_s": round(W * H * args.spp * args.steps / elapsed, 1),
             "render_kernel_ms_avg": round(kernel_ms_avg, 3), "render_kernel_ms_max_over_ranks": round(kernel_ms_max, 3),
-            "roofline": roofline, "roofline_valu": roofline_valu, "cpu_baseline": cpu,
+            "roofline": roofline, "roofline_valu": roofline_valu, "cpu_baseline": cpu, "parity": parity,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

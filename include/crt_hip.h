@@ -129,6 +129,11 @@ typedef struct crt_scene_stats {
     int64_t device_bytes;      /* node + prim + material bytes resident in HBM */
     int32_t max_depth;         /* deepest node (scene + mesh levels) */
     int32_t n_materials;
+    int32_t bvh;               /* CRT_BVH_REFERENCE | CRT_BVH_REBUILT */
+    int32_t layouts;           /* threaded node orders resident (device_nodes counts all of them) */
+    int64_t excluded_prims;    /* REBUILT: triangles the reference can never hit (zero-thickness boxes) */
+    int32_t width;             /* 2 (threaded binary nodes) or 4 (4-wide nodes) */
+    int32_t stack_bound;       /* width 4: traversal-stack entries a ray can need */
 } crt_scene_stats;
 
 typedef struct crt_work_counters {  /* filled by a CRT_RENDER_COUNT_WORK render */
@@ -150,10 +155,47 @@ int crt_abi_version(void);
 const char* crt_last_error(void);   /* thread-local message of the last failing call */
 int crt_device_count(int* out);
 
+/* Acceleration structure the device scene is traversed with.
+ *   CRT_BVH_REFERENCE — the reference's own scene + mesh BVHs, flattened unchanged (default).  Bit-exact:
+ *     same boxes, same visiting order, same culling, same work counters as BVHNode::hit / Mesh::hit.
+ *   CRT_BVH_REBUILT   — a binned-SAH BVH over the same primitives with small padded leaves, emitted in
+ *     six direction-ordered threaded layouts (one per dominant ray axis and sign).  Same hit rule as the
+ *     reference: closest t in [0.001, closest], ties to the primitive the reference visits LAST
+ *     (every primitive carries its reference DFS rank), primitives the reference can never reach
+ *     (inside a zero-thickness box) excluded.  Results differ from the reference only where the
+ *     reference's unpadded boxes round away a genuine hit; see DESIGN.md §4b for the measured rate. */
+#define CRT_BVH_REFERENCE 0
+#define CRT_BVH_REBUILT   1
+
+typedef struct crt_scene_options {
+    int32_t bvh;              /* CRT_BVH_REFERENCE | CRT_BVH_REBUILT */
+    int32_t leaf_size;        /* REBUILT: max triangles per leaf, 1..16 (0 = default 4) */
+    int32_t layouts;          /* REBUILT: 1 (single left-first order) or 6 (direction-ordered, default) */
+    float traversal_cost;     /* REBUILT: SAH cost of one node step relative to one triangle test (0 = default) */
+    int32_t width;            /* REBUILT: 4 (default) = 4-wide nodes, stack traversal (kernel variant 4);
+                                 2 = threaded binary layouts (variants 0-3) */
+    int32_t reserved[3];
+} crt_scene_options;
+
 /* ---- scene (SceneManager device half) ---- */
+/* Host-only: build the device arrays crt_scene_create_ex would upload and copy them out (no GPU needed;
+ * used by the CPU tests to validate the rebuilt BVH).  Call with null arrays to get the sizes:
+ * info = {node float4s, prim float4s, ranks, nodes per layout, layouts, width, stack bound, excluded}. */
+int  crt_scene_export(const crt_scene_desc* desc, const crt_scene_options* opts, float* nodes, float* prims,
+                      int32_t* rank_code, int64_t info[8]);
 int  crt_scene_create(const crt_scene_desc* desc, int device, crt_scene** out);
+/* crt_scene_create with options (NULL = defaults = CRT_BVH_REFERENCE). */
+int  crt_scene_create_ex(const crt_scene_desc* desc, int device, const crt_scene_options* opts, crt_scene** out);
 int  crt_scene_get_stats(const crt_scene* scene, crt_scene_stats* out);
 void crt_scene_destroy(crt_scene* scene);
+
+/* Diagnostic (no reference counterpart): renders spp samples per pixel following scene A (the
+ * renderer's RNG state is consumed, its framebuffer is left untouched) and traces every ray through
+ * scene B as well.  out = {rays, rays whose hit primitive differs, rays with the same primitive but a
+ * different t, of the differing rays those B misses, those A misses}.  Both scenes must come from the
+ * same crt_scene_desc.  Synchronous. */
+int  crt_scene_compare(crt_renderer* r, const crt_scene* a, const crt_scene* b, int spp, int max_bounces,
+                       uint64_t out[5]);
 
 /* ---- renderer (CUDARenderer) ---- */
 int  crt_renderer_create(int width, int height, int device, crt_renderer** out);
@@ -162,14 +204,19 @@ void crt_renderer_destroy(crt_renderer* r);
  * subsequence_base = shard * width * height for spp sharding. */
 int  crt_renderer_init_rand(crt_renderer* r, unsigned long long seed, unsigned long long subsequence_base, void* stream);
 int  crt_renderer_set_camera(crt_renderer* r, const crt_camera_desc* cam);
-/* Render-kernel variant (identical results, different wave scheduling; default 3): 0 = per-lane BVH
- * traversal with per-lane leaf loops; 1 = per-lane traversal with wave-cooperative leaf intersection;
- * 2 = 1 + traversal-step scheduling with parked-lane regeneration (lanes start their next ray
- * without waiting for the wave's slowest trace); 3 = 2 + next-node prefetch overlapping the leaf rounds. */
+/* Render-kernel variant for scenes with threaded binary nodes (identical results, different wave
+ * scheduling; default 3): 0 = per-lane BVH traversal with per-lane leaf loops; 1 = per-lane traversal
+ * with wave-cooperative leaf intersection; 2 = 1 + traversal-step scheduling with parked-lane
+ * regeneration (lanes start their next ray without waiting for the wave's slowest trace); 3 = 2 +
+ * next-node prefetch overlapping the leaf rounds.  Scenes with 4-wide nodes (CRT_BVH_REBUILT, width 4)
+ * always use variant 4: the variant-3 scheduling over 4-wide nodes with a per-lane stack. */
 int  crt_renderer_set_kernel_variant(crt_renderer* r, int variant);
-/* Variant 2: number of parked lanes (1..64, default 32) that triggers a shading/regeneration pass. */
+/* Variants 2-4: number of parked lanes (1..64, default 24) that triggers a shading/regeneration pass. */
 int  crt_renderer_set_regen_threshold(crt_renderer* r, int lanes);
-/* Variant 2: register-allocation occupancy target in waves per SIMD (1 = compiler default, 5, 6, 8). */
+/* Variant 4: per-lane traversal-stack entries kept in LDS (1..16, default 16); deeper entries spill to a
+ * per-pixel region in HBM.  Results do not depend on it (tests force the HBM path with 1). */
+int  crt_renderer_set_stack_lds(crt_renderer* r, int entries);
+/* Variants 2-4: register-allocation occupancy target in waves per SIMD (1 = compiler default, 4-8). */
 int  crt_renderer_set_occupancy_target(crt_renderer* r, int waves_per_simd);
 /* Trace `spp` samples per pixel continuing each pixel's RNG stream; the per-pixel
  * linear sum (pixel_color, CUDAKernels.h:157-162) is kept in an fp32 W*H*3 buffer. */

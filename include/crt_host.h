@@ -26,6 +26,8 @@ void crth_scene_destroy(crth_scene* s);
 int crth_scene_desc(const crth_scene* s, crt_scene_desc* out);
 /* Upload to `device` (crt_scene_create on the desc). */
 int crth_scene_upload(const crth_scene* s, int device, crt_scene** out);
+/* crth_scene_upload with crt_scene_options (NULL = CRT_BVH_REFERENCE). */
+int crth_scene_upload_ex(const crth_scene* s, int device, const crt_scene_options* opts, crt_scene** out);
 
 /* Loader output before the BVH permutation, for parity tests against the oracle loader.
  * counts_out: n_meshes, n_slots, n_indices, n_faces, n_materials (5 x int64). */

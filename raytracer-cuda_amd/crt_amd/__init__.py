@@ -101,10 +101,47 @@ class HostScene:
         fm = np.ctypeslib.as_array(C.cast(d.face_materials, C.POINTER(C.c_int32)), (d.n_faces,)).copy()
         return idx, fm
 
-    def upload(self, device: int = 0) -> "Scene":
+    def upload(self, device: int = 0, bvh: str = "reference", leaf_size: int = 0, layouts: int = 0,
+               traversal_cost: float = 0.0, width: int = 0) -> "Scene":
+        """Device scene.  bvh="reference": the reference's BVHs, bit-exact (crth_scene_upload);
+        bvh="rebuilt": binned-SAH BVH with the reference's hit rule (crt_scene_create_ex)."""
         h = C.c_void_p()
-        check_host(_lib.host().crth_scene_upload(self.h, int(device), C.byref(h)), "crth_scene_upload")
+        if bvh == "reference" and not leaf_size and not layouts and not traversal_cost and not width:
+            check_host(_lib.host().crth_scene_upload(self.h, int(device), C.byref(h)), "crth_scene_upload")
+            return Scene(h, device)
+        o = scene_options(bvh, leaf_size, layouts, traversal_cost, width)
+        d = self.desc()
+        check(_lib.hip().crt_scene_create_ex(C.byref(d), int(device), C.byref(o), C.byref(h)), "crt_scene_create_ex")
         return Scene(h, device)
+
+    def export(self, bvh: str = "reference", **options) -> dict:
+        """The device arrays crt_scene_create_ex would upload (host only, crt_scene_export)."""
+        o = scene_options(bvh, **options)
+        d = self.desc()
+        info = (C.c_int64 * 8)()
+        check(_lib.hip().crt_scene_export(C.byref(d), C.byref(o), None, None, None, info), "crt_scene_export")
+        nodes = np.zeros((info[0], 4), np.float32)
+        prims = np.zeros((info[1], 4), np.float32)
+        rank_code = np.zeros(info[2], np.int32)
+        check(_lib.hip().crt_scene_export(C.byref(d), C.byref(o), _p(nodes), _p(prims), _p(rank_code), info),
+              "crt_scene_export")
+        keys = ("node_float4s", "prim_float4s", "ranks", "nodes_per_layout", "layouts", "width", "stack_bound",
+                "excluded")
+        out = dict(zip(keys, (int(v) for v in info)))
+        out.update(nodes=nodes, prims=prims, rank_code=rank_code)
+        return out
+
+
+def scene_options(bvh: str = "reference", leaf_size: int = 0, layouts: int = 0, traversal_cost: float = 0.0,
+                  width: int = 0):
+    modes = {"reference": _lib.BVH_REFERENCE, "rebuilt": _lib.BVH_REBUILT}
+    if bvh not in modes:
+        raise ValueError(f"bvh must be one of {sorted(modes)}")
+    o = _lib.SceneOptions()
+    o.bvh, o.leaf_size, o.layouts = modes[bvh], int(leaf_size), int(layouts)
+    o.traversal_cost = float(traversal_cost)
+    o.width = int(width)
+    return o
 
 
 def _nodes_to_np(ptr, n):
@@ -135,9 +172,9 @@ class Scene:
     __del__ = close
 
 
-def load_scene(obj_files, device: int = 0):
+def load_scene(obj_files, device: int = 0, **upload_options):
     hs = HostScene(obj_files)
-    return hs, hs.upload(device)
+    return hs, hs.upload(device, **upload_options)
 
 
 class Renderer:
@@ -166,6 +203,9 @@ class Renderer:
 
     def set_regen_threshold(self, lanes: int):
         check(_lib.hip().crt_renderer_set_regen_threshold(self.h, int(lanes)), "set_regen_threshold")
+
+    def set_stack_lds(self, entries: int):
+        check(_lib.hip().crt_renderer_set_stack_lds(self.h, int(entries)), "set_stack_lds")
 
     def set_camera(self, cam: CameraDesc):
         self._cam = cam
@@ -229,6 +269,15 @@ class Renderer:
         self.render(scene, spp, max_bounces, stream=stream)
         self.resolve(pixel_sample_scale(spp), stream)
         self.synchronize(stream)
+
+    def compare(self, scene_a: Scene, scene_b: Scene, spp: int, max_bounces: int = 20) -> dict:
+        """Per-ray hit agreement of two device scenes (crt_scene_compare); paths follow scene_a.
+        Call init_rand first; the RNG state is consumed."""
+        out = (C.c_uint64 * 5)()
+        check(_lib.hip().crt_scene_compare(self.h, scene_a.h, scene_b.h, int(spp), int(max_bounces), out),
+              "crt_scene_compare")
+        keys = ("rays", "rank_mismatch", "t_mismatch", "b_miss", "a_miss")
+        return dict(zip(keys, (int(v) for v in out)))
 
 
 def pixel_sample_scale(spp: int) -> float:

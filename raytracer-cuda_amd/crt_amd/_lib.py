@@ -54,7 +54,17 @@ class MeshDesc(C.Structure):
 
 class SceneStats(C.Structure):
     _fields_ = [("device_nodes", C.c_int64), ("device_prims", C.c_int64), ("device_bytes", C.c_int64),
-                ("max_depth", C.c_int32), ("n_materials", C.c_int32)]
+                ("max_depth", C.c_int32), ("n_materials", C.c_int32), ("bvh", C.c_int32), ("layouts", C.c_int32),
+                ("excluded_prims", C.c_int64), ("width", C.c_int32), ("stack_bound", C.c_int32)]
+
+
+class SceneOptions(C.Structure):
+    _fields_ = [("bvh", C.c_int32), ("leaf_size", C.c_int32), ("layouts", C.c_int32),
+                ("traversal_cost", C.c_float), ("width", C.c_int32), ("reserved", C.c_int32 * 3)]
+
+
+BVH_REFERENCE = 0
+BVH_REBUILT = 1
 
 
 class WorkCounters(C.Structure):
@@ -64,7 +74,8 @@ class WorkCounters(C.Structure):
 
 # exported symbol lists (checked by tests against include/*.h)
 HIP_SYMBOLS = [
-    "crt_abi_version", "crt_last_error", "crt_device_count", "crt_scene_create", "crt_scene_get_stats",
+    "crt_abi_version", "crt_last_error", "crt_device_count", "crt_scene_create", "crt_scene_create_ex", "crt_scene_get_stats", "crt_scene_compare", "crt_scene_export",
+    "crt_renderer_set_stack_lds",
     "crt_scene_destroy", "crt_renderer_create", "crt_renderer_destroy", "crt_renderer_init_rand",
     "crt_renderer_set_camera", "crt_renderer_render", "crt_renderer_resolve", "crt_renderer_render_frame",
     "crt_renderer_synchronize", "crt_renderer_read_linear", "crt_renderer_read_rgba8", "crt_renderer_read_rng",
@@ -75,7 +86,7 @@ HIP_SYMBOLS = [
     "crt_selftest_math", "crt_selftest_rng", "crt_selftest_scan", "crt_selftest_rcp",
 ]
 HOST_SYMBOLS = [
-    "crth_scene_load", "crth_scene_destroy", "crth_scene_desc", "crth_scene_upload", "crth_scene_counts",
+    "crth_scene_load", "crth_scene_destroy", "crth_scene_desc", "crth_scene_upload", "crth_scene_upload_ex", "crth_scene_counts",
     "crth_scene_loader_arrays", "crth_camera", "crth_last_error",
 ]
 
@@ -109,7 +120,9 @@ def hip():
         sig = {
             "crt_abi_version": ([], i32), "crt_last_error": ([], C.c_char_p),
             "crt_device_count": ([P], i32),
-            "crt_scene_create": ([P, i32, P], i32), "crt_scene_get_stats": ([P, P], i32),
+            "crt_scene_create": ([P, i32, P], i32), "crt_scene_create_ex": ([P, i32, P, P], i32),
+            "crt_scene_compare": ([P, P, P, i32, i32, P], i32),
+            "crt_scene_export": ([P, P, P, P, P, P], i32), "crt_renderer_set_stack_lds": ([P, i32], i32), "crt_scene_get_stats": ([P, P], i32),
             "crt_scene_destroy": ([P], None),
             "crt_renderer_create": ([i32, i32, i32, P], i32), "crt_renderer_destroy": ([P], None),
             "crt_renderer_init_rand": ([P, u64, u64, P], i32), "crt_renderer_set_camera": ([P, P], i32),
@@ -150,6 +163,7 @@ def host():
         sig = {
             "crth_scene_load": ([P, i32, P], i32), "crth_scene_destroy": ([P], None),
             "crth_scene_desc": ([P, P], i32), "crth_scene_upload": ([P, i32, P], i32),
+            "crth_scene_upload_ex": ([P, i32, P, P], i32),
             "crth_scene_counts": ([P, P], i32), "crth_scene_loader_arrays": ([P, P, P, P, P, P], i32),
             "crth_camera": ([f32, f32, P, P, f32, f32, f32, f32, i32, P], i32),
             "crth_last_error": ([], C.c_char_p),

@@ -26,9 +26,13 @@ namespace crt {
 //   sphere leaf        : a = 0, b = SPHERE_BIT | sphere prim          (scene level: [0.001, inf))
 //   every leaf continues at node + 1.
 // prims: 3 x float4 (48 B) per primitive.
-//   triangle: (v0.xyz, e1.x) (e1.y, e1.z, e2.xy) (e2.z, material, 0, 0)   e1 = v1-v0, e2 = v2-v0
+//   triangle: (v0.xyz, e1.x) (e1.y, e1.z, e2.xy) (e2.z, material, rank, 0)   e1 = v1-v0, e2 = v2-v0
 //             (bit-identical to Mesh.cuh:277-278, which subtracts in f32 too)
-//   sphere  : (center.xyz, radius) (radius^2, material, 0, 0) (0,0,0,0)
+//   sphere  : (center.xyz, radius) (radius^2, material, rank, 0) (0,0,0,0)
+//   rank = position of the primitive in the reference's DFS visiting order (ties go to the higher rank);
+//   rank_code[rank] = prim index (| SPHERE_BIT for spheres) maps a hit back to its record.
+// CRT_BVH_REBUILT scenes hold 1 or 6 threaded layouts of the same tree back to back (n_nodes each; skip
+// links relative to the layout); internal nodes are NODE_MESH_INNER, leaves as above.
 // materials: 3 x float4 (48 B): (type, albedo.xyz) (emission.xyz, roughness) (ior, 0, 0, 0)
 constexpr int NODE_MESH_INNER = -1;
 constexpr int NODE_SCENE_INNER = -3;

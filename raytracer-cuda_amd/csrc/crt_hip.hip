@@ -20,6 +20,7 @@
 
 #include "crt_hip.h"
 #include "crt_device.h"
+#include "crt_sah.h"
 
 using namespace crt;
 
@@ -41,7 +42,12 @@ struct RenderParams {
     const float4* __restrict__ nodes;
     const float4* __restrict__ prims;
     const float4* __restrict__ mats;
-    int n_nodes, n_mats, n_prims;
+    const int* __restrict__ rank_code;   // reference DFS rank -> prim code (prim index, SPHERE_BIT for spheres)
+    int n_nodes, n_mats, n_prims;         // n_nodes: nodes of ONE threaded layout
+    int n_layouts;                        // 1, or 6 direction-ordered layouts (CRT_BVH_REBUILT)
+    uint32_t* __restrict__ ovf;           // variant 4: traversal-stack entries beyond the LDS part
+    int stack_cap;                        // variant 4: stack entries a ray can need (host bound)
+    int stack_lds;                        // variant 4: entries kept in LDS (<= STACK_LDS; rest in ovf)
     unsigned* err;                // device error flag (bit 0: primitive index out of range)
     int width, height, spp, max_bounces;
     int accumulate;
@@ -54,15 +60,33 @@ struct RenderParams {
 
 struct TraceCounts { uint32_t boxes, tris, spheres, step_slots, round_slots, trace_calls; };
 
-// Closest hit over the threaded scene+mesh BVH.  Returns hit prim (SPHERE_BIT set for
-// spheres) or -1; `closest` = IntersectionTime of the accepted hit.
+// Hit rule shared by every variant and both BVH modes: a candidate (t, rank) replaces the current hit
+// when t < closest, or t == closest and its reference DFS rank is higher.  In CRT_BVH_REFERENCE mode the
+// traversal visits primitives in rank order, so this is exactly the reference's closed-interval
+// acceptance (ties go to the later primitive); in CRT_BVH_REBUILT mode it reproduces that choice in
+// any visiting order.
+__device__ __forceinline__ bool better(float t, int rank, float closest, int hit) {
+    return t < closest || (t == closest && rank > hit);
+}
+
+// Node array offset (in float4) of the threaded layout a ray walks: layout 2*axis + (d[axis] < 0) for the
+// dominant axis of d when six direction-ordered layouts are resident, else 0.
+__device__ __forceinline__ int layout_base(V3 d, int n_layouts, int n_nodes) {
+    if (n_layouts == 1) return 0;
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    const int l = (ax >= ay && ax >= az) ? (d.x < 0.f) : (ay >= az ? 2 + (d.y < 0.f) : 4 + (d.z < 0.f));
+    return 2 * l * n_nodes;
+}
+
+// Closest hit over the threaded scene+mesh BVH.  Returns the reference DFS rank of the hit primitive
+// or -1; `closest` = IntersectionTime of the accepted hit.
 // Semantics: BVHNode::hit (BVHNode.cuh:304-345), Mesh::hit (Mesh.cuh:55-110),
 // AABB::hit (AABB.cuh:123-146), rayTriangleIntersect (Mesh.cuh:266-308),
 // Sphere::hit (Sphere.cuh:27-47); closed-interval acceptance so ties go to the
 // later primitive, exactly as in the reference order.
 template <bool COUNT>
 __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const float4* __restrict__ prims,
-                                     int n_nodes, V3 o, V3 d, float& closest, TraceCounts& cnt) {
+                                     int n_nodes, int nbase, V3 o, V3 d, float& closest, TraceCounts& cnt) {
     const float INF = __builtin_inff();
     // AABB::hit computes 1/d per node visit; the value is the same every time.
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -70,8 +94,8 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
     int hit = -1;
     int node = 0;
     while (node < n_nodes) {
-        const float4 A = nodes[2 * node];
-        const float4 B = nodes[2 * node + 1];
+        const float4 A = nodes[nbase + 2 * node];
+        const float4 B = nodes[nbase + 2 * node + 1];
         const int a = __float_as_int(B.z);
         const int b = __float_as_int(B.w);
         const bool scene_level = (b == NODE_SCENE_INNER) || (b >= SPHERE_BIT);
@@ -105,7 +129,8 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
                         root = (-hb + sq) / qa;
                         if (root < 0.001f || root > closest) ok = false;
                     }
-                    if (ok) { closest = root; hit = b; }
+                    const int rank = __float_as_int(f1.z);
+                    if (ok && better(root, rank, closest, hit)) { closest = root; hit = rank; }
                 }
             } else {
                 for (int k = 0; k < a; ++k) {
@@ -126,8 +151,10 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
                     if (v < 0.f || (u + v) > 1.f) continue;
                     const float t = f * dot(e2, q);
                     if (t < 0.001f || t > closest) continue;
+                    const int rank = __float_as_int(f2.z);
+                    if (!better(t, rank, closest, hit)) continue;
                     closest = t;
-                    hit = p;
+                    hit = rank;
                 }
             }
         }
@@ -186,14 +213,14 @@ __device__ __forceinline__ int wave_inclusive_scan_shfl(int x, int lane) {
 struct WaveLds {
     float4 ray0[64];                 // o.x, o.y, o.z, d.x of each lane's ray
     float4 ray1[64];                 // d.y, d.z, closest at leaf entry, first prim (int bits)
-    unsigned long long key[64];      // per owner: (t bits << 32) | (0xffffffff - k), min-reduced
+    unsigned long long key[64];      // per owner: (t bits << 32) | (0xffffffff - rank), min-reduced
     int prefix[64];                  // first pair index of each owner's leaf
     unsigned char owner_at[64];      // owner lane of the pair that starts at each slot of a round
 };
 
-// Möller–Trumbore (Mesh.cuh:266-308) on prim p; returns t or -1 when rejected (any accepted t >= 0.001).
-__device__ __forceinline__ float tri_test(const float4* __restrict__ prims, int p, V3 o, V3 d, float tmax) {
-    const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1], f2 = prims[3 * p + 2];
+// Möller–Trumbore (Mesh.cuh:266-308) on a triangle record; returns t or -1 when rejected (any accepted
+// t >= 0.001).
+__device__ __forceinline__ float tri_test_rec(float4 f0, float4 f1, float4 f2, V3 o, V3 d, float tmax) {
     const V3 e1 = v3(f0.w, f1.x, f1.y);
     const V3 e2 = v3(f1.z, f1.w, f2.x);
     const V3 h = cross(d, e2);
@@ -210,8 +237,40 @@ __device__ __forceinline__ float tri_test(const float4* __restrict__ prims, int 
     if (t < 0.001f || t > tmax) return -1.f;
     return t;
 }
+__device__ __forceinline__ float tri_test(const float4* __restrict__ prims, int p, V3 o, V3 d, float tmax, int& rank) {
+    const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1], f2 = prims[3 * p + 2];
+    rank = __float_as_int(f2.z);
+    return tri_test_rec(f0, f1, f2, o, d, tmax);
+}
 
-// Sphere::hit (Sphere.cuh:27-47) against [0.001, closest]; updates closest/hit on acceptance.
+// Sphere::hit (Sphere.cuh:27-47) as a candidate: the root it would accept against any closest >= the
+// result (the near root if >= 0.001, else the far one), or -1.  Independent of the visiting order, so
+// it can enter the same min-reduction as triangles.
+__device__ __forceinline__ float sphere_candidate(float4 f0, float4 f1, V3 o, V3 d, float tmax) {
+    const V3 oc = o - v3(f0.x, f0.y, f0.z);
+    const float qa = dot(d, d);
+    const float hb = dot(oc, d);
+    const float qc = dot(oc, oc) - f1.x;
+    const float disc = hb * hb - qa * qc;
+    if (disc < 0) return -1.f;
+    const float sq = sqrtf(disc);
+    float root = (-hb - sq) / qa;
+    if (root < 0.001f || root > tmax) {
+        root = (-hb + sq) / qa;
+        if (root < 0.001f || root > tmax) return -1.f;
+    }
+    return root;
+}
+
+// Any primitive of a CRT_BVH_REBUILT leaf: triangle, or sphere (record word 11 == 1).
+__device__ __forceinline__ float prim_test(const float4* __restrict__ prims, int p, V3 o, V3 d, float tmax, int& rank) {
+    const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1], f2 = prims[3 * p + 2];
+    rank = __float_as_int(f2.z);
+    if (__float_as_int(f2.w) == 1) return sphere_candidate(f0, f1, o, d, tmax);
+    return tri_test_rec(f0, f1, f2, o, d, tmax);
+}
+
+// Sphere::hit (Sphere.cuh:27-47) against [0.001, closest]; updates closest/hit (= rank) on acceptance.
 __device__ __forceinline__ void sphere_test(const float4* __restrict__ prims, int b, V3 o, V3 d, float& closest, int& hit) {
     const int p = b - SPHERE_BIT;
     const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1];
@@ -227,8 +286,10 @@ __device__ __forceinline__ void sphere_test(const float4* __restrict__ prims, in
         root = (-hb + sq) / qa;
         if (root < 0.001f || root > closest) return;
     }
+    const int rank = __float_as_int(f1.z);
+    if (!better(root, rank, closest, hit)) return;
     closest = root;
-    hit = b;
+    hit = rank;
 }
 
 // Variant 1: per-lane threaded traversal, leaf triangles tested cooperatively by the whole wave.
@@ -238,7 +299,7 @@ __device__ __forceinline__ void sphere_test(const float4* __restrict__ prims, in
 // the same closest hit (ties to the later triangle) as Mesh::hit's sequential loop.
 // MUST be called by all 64 lanes (inactive lanes pass active=false).
 template <bool COUNT>
-__device__ int trace_coop(const float4* __restrict__ nodes, const float4* __restrict__ prims, int n_nodes,
+__device__ int trace_coop(const float4* __restrict__ nodes, const float4* __restrict__ prims, int n_nodes, int nbase,
                           int n_prims, unsigned* err, V3 o, V3 d, bool active, float& closest, TraceCounts& cnt,
                           WaveLds& L, int lane) {
     const float INF = __builtin_inff();
@@ -253,8 +314,8 @@ __device__ int trace_coop(const float4* __restrict__ nodes, const float4* __rest
         if (COUNT) cnt.step_slots++;        // one traversal step of the wave (x64 lanes)
         int leaf_n = 0, leaf_first = 0;
         if (node < n_nodes) {
-            const float4 A = nodes[2 * node];
-            const float4 B = nodes[2 * node + 1];
+            const float4 A = nodes[nbase + 2 * node];
+            const float4 B = nodes[nbase + 2 * node + 1];
             const int a = __float_as_int(B.z);
             const int b = __float_as_int(B.w);
             const bool scene_level = (b == NODE_SCENE_INNER) || (b >= SPHERE_BIT);
@@ -309,9 +370,10 @@ __device__ int trace_coop(const float4* __restrict__ nodes, const float4* __rest
                 const int p = __float_as_int(r1.w) + k;
                 if (COUNT) cnt.tris++;
                 if ((unsigned)p < (unsigned)n_prims && (unsigned)k < 0xffffffffu) {
-                    const float t = tri_test(prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z);
+                    int rank;
+                    const float t = tri_test(prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank);
                     if (t >= 0.f)
-                        atomicMin(&L.key[owner], ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)k));
+                        atomicMin(&L.key[owner], ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank));
                 } else {
                     atomicOr(err, 1u);                // indexing bug: report instead of faulting
                 }
@@ -321,9 +383,11 @@ __device__ int trace_coop(const float4* __restrict__ nodes, const float4* __rest
         }
         if (leaf_n > 0) {
             const unsigned long long kk = L.key[lane];
-            if (kk != ~0ull) {
-                closest = __uint_as_float((unsigned)(kk >> 32));
-                hit = leaf_first + (int)(0xffffffffu - (unsigned)kk);
+            const float t = __uint_as_float((unsigned)(kk >> 32));
+            const int rank = (int)(0xffffffffu - (unsigned)kk);
+            if (kk != ~0ull && better(t, rank, closest, hit)) {
+                closest = t;
+                hit = rank;
             }
         }
     }
@@ -336,15 +400,15 @@ __device__ int trace_coop(const float4* __restrict__ nodes, const float4* __rest
 // the box test so its latency overlaps this step's leaf rounds.
 template <bool COUNT, bool PREFETCH>
 __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, const float4* __restrict__ prims,
-                                              int n_nodes, int n_prims, unsigned* err, V3 o, V3 d, V3 inv,
-                                              int& node, float& closest, int& hit, TraceCounts& cnt, WaveLds& L,
-                                              int lane, float4& pA, float4& pB) {
+                                              int n_nodes, int nbase, int n_prims, unsigned* err, V3 o, V3 d,
+                                              V3 inv, int& node, float& closest, int& hit, TraceCounts& cnt,
+                                              WaveLds& L, int lane, float4& pA, float4& pB) {
     const float INF = __builtin_inff();
     if (COUNT) cnt.step_slots++;
     int leaf_n = 0, leaf_first = 0;
     if (node < n_nodes) {
-        const float4 A = PREFETCH ? pA : nodes[2 * node];
-        const float4 B = PREFETCH ? pB : nodes[2 * node + 1];
+        const float4 A = PREFETCH ? pA : nodes[nbase + 2 * node];
+        const float4 B = PREFETCH ? pB : nodes[nbase + 2 * node + 1];
         const int a = __float_as_int(B.z);
         const int b = __float_as_int(B.w);
         const bool scene_level = (b == NODE_SCENE_INNER) || (b >= SPHERE_BIT);
@@ -371,8 +435,8 @@ __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, 
         }
         node = next;
         if (PREFETCH && next < n_nodes) {
-            pA = nodes[2 * next];
-            pB = nodes[2 * next + 1];
+            pA = nodes[nbase + 2 * next];
+            pB = nodes[nbase + 2 * next + 1];
         }
     }
     if (!__ballot(leaf_n > 0)) return;
@@ -400,9 +464,10 @@ __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, 
             const int p = __float_as_int(r1.w) + k;
             if (COUNT) cnt.tris++;
             if ((unsigned)p < (unsigned)n_prims) {
-                const float t = tri_test(prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z);
+                int rank;
+                const float t = tri_test(prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank);
                 if (t >= 0.f)
-                    atomicMin(&L.key[owner], ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)k));
+                    atomicMin(&L.key[owner], ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank));
             } else {
                 atomicOr(err, 1u);
             }
@@ -412,9 +477,200 @@ __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, 
     }
     if (leaf_n > 0) {
         const unsigned long long kk = L.key[lane];
-        if (kk != ~0ull) {
-            closest = __uint_as_float((unsigned)(kk >> 32));
-            hit = leaf_first + (int)(0xffffffffu - (unsigned)kk);
+        const float t = __uint_as_float((unsigned)(kk >> 32));
+        const int rank = (int)(0xffffffffu - (unsigned)kk);
+        if (kk != ~0ull && better(t, rank, closest, hit)) {
+            closest = t;
+            hit = rank;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ 4-wide BVH (CRT_BVH_REBUILT)
+// Node = 8 x float4 (128 B): child boxes as SoA rows (lo.x[4], hi.x[4], lo.y[4], hi.y[4], lo.z[4],
+// hi.z[4]), then meta = (first_child, n_internal | n_slots << 8, leaf_first, 8-bit triangle count per
+// slot), then padding.  Slots [0, n_internal) are internal children at node first_child + slot; the
+// following slots are leaves whose primitives are consecutive from leaf_first in slot order; empty slots
+// have a zero-thickness box far away (never hit).
+constexpr int STACK_LDS = 16;   // per-lane traversal-stack entries kept in LDS; deeper entries go to P.ovf
+
+typedef float pf2 __attribute__((ext_vector_type(2)));
+
+struct Wide4 {
+    float tmin[4];
+    bool hit[4];
+};
+
+// Slab test of the four child boxes against [0.001, tmax]; (lo - o) * inv in packed f32 (IEEE per half).
+__device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ q, V3 o, V3 inv, float tmax) {
+    const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
+    const pf2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const pf2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+    const pf2 ax0 = ((pf2){lx.x, lx.y} - ox) * ix, ax1 = ((pf2){lx.z, lx.w} - ox) * ix;
+    const pf2 bx0 = ((pf2){hx.x, hx.y} - ox) * ix, bx1 = ((pf2){hx.z, hx.w} - ox) * ix;
+    const pf2 ay0 = ((pf2){ly.x, ly.y} - oy) * iy, ay1 = ((pf2){ly.z, ly.w} - oy) * iy;
+    const pf2 by0 = ((pf2){hy.x, hy.y} - oy) * iy, by1 = ((pf2){hy.z, hy.w} - oy) * iy;
+    const pf2 az0 = ((pf2){lz.x, lz.y} - oz) * iz, az1 = ((pf2){lz.z, lz.w} - oz) * iz;
+    const pf2 bz0 = ((pf2){hz.x, hz.y} - oz) * iz, bz1 = ((pf2){hz.z, hz.w} - oz) * iz;
+    const float ax[4] = {ax0.x, ax0.y, ax1.x, ax1.y}, bx[4] = {bx0.x, bx0.y, bx1.x, bx1.y};
+    const float ay[4] = {ay0.x, ay0.y, ay1.x, ay1.y}, by[4] = {by0.x, by0.y, by1.x, by1.y};
+    const float az[4] = {az0.x, az0.y, az1.x, az1.y}, bz[4] = {bz0.x, bz0.y, bz1.x, bz1.y};
+    Wide4 w;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const float t0 = fmaxf(fmaxf(fminf(ax[s], bx[s]), fminf(ay[s], by[s])), fmaxf(fminf(az[s], bz[s]), 0.001f));
+        const float t1 = fminf(fminf(fmaxf(ax[s], bx[s]), fmaxf(ay[s], by[s])), fminf(fmaxf(az[s], bz[s]), tmax));
+        w.tmin[s] = t0;
+        w.hit[s] = t0 < t1;
+    }
+    return w;
+}
+
+__device__ __forceinline__ void cas(uint32_t& a, uint32_t& b) {
+    const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+
+// Per-lane closest hit over a 4-wide BVH (diagnostic path: crt_scene_compare).  Returns the rank or -1.
+__device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict__ prims, V3 o, V3 d,
+                      float& closest) {
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    closest = __builtin_inff();
+    int hit = -1, node = 0, sp = 0;
+    int stack[64];
+    while (node >= 0) {
+        const float4* q = nodes + 8 * (size_t)node;
+        const Wide4 w = wide_boxes(q, o, inv, closest);
+        const float4 mf = q[6];
+        const int first_child = __float_as_int(mf.x), n_int = __float_as_int(mf.y) & 0xff;
+        const uint32_t counts = __float_as_uint(mf.w);
+        int off = 0;
+        const float entry = closest;
+        for (int s = 0; s < 4; ++s) {
+            const int c = (counts >> (8 * s)) & 0xff;
+            if (s >= n_int && c > 0 && w.hit[s]) {
+                for (int k = 0; k < c; ++k) {
+                    int rank;
+                    const float t = prim_test(prims, __float_as_int(mf.z) + off + k, o, d, entry, rank);
+                    if (t >= 0.f && better(t, rank, closest, hit)) { closest = t; hit = rank; }
+                }
+            }
+            off += c;
+        }
+        uint32_t k[4];
+        for (int s = 0; s < 4; ++s) k[s] = (s < n_int && w.hit[s]) ? ((__float_as_uint(w.tmin[s]) & ~3u) | s) : ~0u;
+        cas(k[0], k[1]); cas(k[2], k[3]); cas(k[0], k[2]); cas(k[1], k[3]); cas(k[1], k[2]);
+        if (k[0] != ~0u) {
+            node = first_child + (int)(k[0] & 3);
+            for (int s = 3; s >= 1; --s)
+                if (k[s] != ~0u && sp < 64) stack[sp++] = first_child + (int)(k[s] & 3);
+        } else {
+            node = sp > 0 ? stack[--sp] : -1;
+        }
+    }
+    return hit;
+}
+
+// One wave traversal step over a 4-wide BVH (variant 4).  Every lane with a node tests its four child
+// boxes; hit internal children are ordered near-first (u32 sort of (tmin bits | slot) keys), the nearest
+// becomes the lane's next node and the others are pushed onto its stack; the primitives of the hit leaf
+// children (one consecutive range) join this step's cooperative leaf rounds.  All 64 lanes call it.
+template <bool COUNT>
+__device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d, V3 inv, int& node, int& sp,
+                                               float& closest, int& hit, TraceCounts& cnt, WaveLds& L,
+                                               uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix) {
+    if (COUNT) cnt.step_slots++;
+    int leaf_n = 0, leaf_first = 0;
+    if (node >= 0) {
+        const float4* q = P.nodes + 8 * (size_t)node;
+        const float4 mf = q[6];
+        const Wide4 w = wide_boxes(q, o, inv, closest);
+        const int first_child = __float_as_int(mf.x);
+        const int meta = __float_as_int(mf.y);
+        const uint32_t counts = __float_as_uint(mf.w);
+        const int n_int = meta & 0xff;
+        if (COUNT) cnt.boxes += (uint32_t)(meta >> 8);
+        // leaf children: consecutive primitives; test the span from the first to the last hit leaf
+        const int c0 = counts & 0xff, c1 = (counts >> 8) & 0xff, c2 = (counts >> 16) & 0xff, c3 = counts >> 24;
+        const int off[4] = {0, c0, c0 + c1, c0 + c1 + c2};
+        const int cc[4] = {c0, c1, c2, c3};
+        int lo = 0x7fffffff, hi = 0;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const bool lh = s >= n_int && cc[s] > 0 && w.hit[s];
+            lo = lh ? min(lo, off[s]) : lo;
+            hi = lh ? max(hi, off[s] + cc[s]) : hi;
+        }
+        if (hi > lo) {
+            leaf_n = hi - lo;
+            leaf_first = __float_as_int(mf.z) + lo;
+        }
+        uint32_t k[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) k[s] = (s < n_int && w.hit[s]) ? ((__float_as_uint(w.tmin[s]) & ~3u) | s) : ~0u;
+        cas(k[0], k[1]); cas(k[2], k[3]); cas(k[0], k[2]); cas(k[1], k[3]); cas(k[1], k[2]);
+        auto push = [&](uint32_t v) {
+            if (sp < P.stack_lds) stk[sp * 64 + lane] = v;
+            else if (sp < P.stack_cap) P.ovf[(size_t)(sp - P.stack_lds) * n_pix + pix] = v;
+            else atomicOr(P.err, 2u);        // host stack bound violated: report, drop the entry
+            ++sp;
+        };
+        if (k[0] != ~0u) {
+            node = first_child + (int)(k[0] & 3);
+            if (k[3] != ~0u) push((uint32_t)first_child + (k[3] & 3));
+            if (k[2] != ~0u) push((uint32_t)first_child + (k[2] & 3));
+            if (k[1] != ~0u) push((uint32_t)first_child + (k[1] & 3));
+        } else if (sp > 0) {
+            --sp;
+            node = sp < P.stack_lds ? (int)stk[sp * 64 + lane]
+                                    : (sp < P.stack_cap ? (int)P.ovf[(size_t)(sp - P.stack_lds) * n_pix + pix] : -1);
+        } else {
+            node = -1;
+        }
+    }
+    if (!__ballot(leaf_n > 0)) return;
+    const int incl = wave_inclusive_scan(leaf_n, lane);
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    const int pfx = incl - leaf_n;
+    if (leaf_n > 0) {
+        L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first));
+        L.prefix[lane] = pfx;
+        L.key[lane] = ~0ull;
+    }
+    int carry = 0;
+    for (int base = 0; base < total; base += 64) {
+        if (COUNT) cnt.round_slots++;
+        if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)lane;
+        wave_sync();
+        const int mark = L.owner_at[lane];
+        L.owner_at[lane] = 0xff;
+        int owner = wave_inclusive_max_scan(mark == 0xff ? -1 : mark, lane);
+        owner = owner > carry ? owner : carry;
+        const int j = base + lane;
+        if (j < total) {
+            const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
+            const int p = __float_as_int(r1.w) + (j - L.prefix[owner]);
+            if (COUNT) cnt.tris++;
+            if ((unsigned)p < (unsigned)P.n_prims) {
+                int rank;
+                const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank);
+                if (t >= 0.f)
+                    atomicMin(&L.key[owner], ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank));
+            } else {
+                atomicOr(P.err, 1u);
+            }
+        }
+        carry = __builtin_amdgcn_readlane(owner, 63);
+        wave_sync();
+    }
+    if (leaf_n > 0) {
+        const unsigned long long kk = L.key[lane];
+        const float t = __uint_as_float((unsigned)(kk >> 32));
+        const int rank = (int)(0xffffffffu - (unsigned)kk);
+        if (kk != ~0ull && better(t, rank, closest, hit)) {
+            closest = t;
+            hit = rank;
         }
     }
 }
@@ -480,13 +736,14 @@ __device__ __forceinline__ bool next_ray(PathState& S, const CamRegs& C, int x, 
 }
 
 // Phase 3: material scatter / emit / sky (CUDAKernels.h:123-142, Material.cuh:66-146).
-__device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int hit, float t) {
-    if (hit < 0) {                                       // :137-142
+__device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int hit_rank, float t) {
+    if (hit_rank < 0) {                                  // :137-142
         S.pixel = S.pixel + S.thr * sky(S.d);
         ++S.paths;
         S.need_new = true;
         return;
     }
+    const int hit = P.rank_code[hit_rank];
     const V3 hp = S.o + t * S.d;                         // Ray::pointAtDistance
     V3 outward;
     uint32_t mat;
@@ -557,6 +814,7 @@ __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int h
 template <bool COUNT, int VARIANT, int MINW>
 __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
     __shared__ WaveLds lds[VARIANT >= 1 ? 4 : 1];
+    __shared__ uint32_t stack_lds[VARIANT == 4 ? 4 * STACK_LDS * 64 : 1];
     // 16x16 pixel tile per workgroup, 8x8 per wave64.
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -594,8 +852,46 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
             if (!next_ray(S, C, x, y, P.max_bounces)) break;
             ++S.rays;
             float t;
-            const int hit = trace<COUNT>(P.nodes, P.prims, P.n_nodes, S.o, S.d, t, cnt);
+            const int hit = trace<COUNT>(P.nodes, P.prims, P.n_nodes, layout_base(S.d, P.n_layouts, P.n_nodes), S.o,
+                                         S.d, t, cnt);
             shade(S, P, hit, t);
+        }
+    } else if (VARIANT == 4) {
+        // Same scheduling as variant 3 over a 4-wide BVH: node < 0 = no node left (lane parked).
+        WaveLds& L = lds[wave];
+        uint32_t* stk = stack_lds + wave * STACK_LDS * 64;
+        const float INF = __builtin_inff();
+        const size_t n_pix = (size_t)P.width * P.height;
+        bool live = true, has_result = false;
+        int node = -1, sp = 0, hit = -1;
+        float closest = INF;
+        V3 inv = v3(0.f, 0.f, 0.f);
+        L.owner_at[lane] = 0xff;
+        for (;;) {
+            const bool parked = live && node < 0;
+            const int n_parked = __popcll(__ballot(parked));
+            const int n_live = __popcll(__ballot(live));
+            if (n_live == 0) break;
+            if (n_parked >= P.regen_threshold || n_parked == n_live) {
+                if (parked) {
+                    if (has_result) shade(S, P, hit, closest);
+                    live = next_ray(S, C, x, y, P.max_bounces);
+                    has_result = false;
+                    if (live) {
+                        ++S.rays;
+                        has_result = true;
+                        node = 0;
+                        sp = 0;
+                        closest = INF;
+                        hit = -1;
+                        // conservative traversal only needs 1/d to within an ulp (boxes are padded)
+                        inv = v3(__builtin_amdgcn_rcpf(S.d.x), __builtin_amdgcn_rcpf(S.d.y), __builtin_amdgcn_rcpf(S.d.z));
+                        L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
+                        if (COUNT) cnt.trace_calls++;
+                    }
+                }
+            }
+            traverse_step4<COUNT>(P, S.o, S.d, inv, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
         }
     } else if (VARIANT == 2 || VARIANT == 3) {
         constexpr bool PF = VARIANT == 3;
@@ -606,7 +902,7 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
         WaveLds& L = lds[wave];
         const float INF = __builtin_inff();
         bool live = true, has_result = false;
-        int node = P.n_nodes, hit = -1;
+        int node = P.n_nodes, hit = -1, nbase = 0;
         float closest = INF;
         V3 inv = v3(0.f, 0.f, 0.f);
         L.owner_at[lane] = 0xff;
@@ -627,17 +923,18 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
                         closest = INF;
                         hit = -1;
                         inv = v3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
+                        nbase = layout_base(S.d, P.n_layouts, P.n_nodes);
                         L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                         if (PF) {
-                            pA = P.nodes[0];
-                            pB = P.nodes[1];
+                            pA = P.nodes[nbase];
+                            pB = P.nodes[nbase + 1];
                         }
                         if (COUNT) cnt.trace_calls++;
                     }
                 }
             }
-            traverse_step<COUNT, PF>(P.nodes, P.prims, P.n_nodes, P.n_prims, P.err, S.o, S.d, inv, node, closest,
-                                     hit, cnt, L, lane, pA, pB);
+            traverse_step<COUNT, PF>(P.nodes, P.prims, P.n_nodes, nbase, P.n_prims, P.err, S.o, S.d, inv, node,
+                                     closest, hit, cnt, L, lane, pA, pB);
         }
     } else {
         bool live = true;
@@ -645,8 +942,8 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
             if (live) live = next_ray(S, C, x, y, P.max_bounces);
             if (!__ballot(live)) break;
             float t;
-            const int hit = trace_coop<COUNT>(P.nodes, P.prims, P.n_nodes, P.n_prims, P.err, S.o, S.d, live, t, cnt,
-                                              lds[wave], lane);
+            const int hit = trace_coop<COUNT>(P.nodes, P.prims, P.n_nodes, layout_base(S.d, P.n_layouts, P.n_nodes),
+                                              P.n_prims, P.err, S.o, S.d, live, t, cnt, lds[wave], lane);
             if (live) {
                 ++S.rays;
                 shade(S, P, hit, t);
@@ -677,6 +974,69 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
         }
     }
     if (lane == 0) atomicAdd(&P.counters[0], (unsigned long long)wr);
+}
+
+// Diagnostic: paths follow scene A (variant-0 trace); every ray is ALSO traced through scene B and the two
+// closest hits compared.  counters: [0] rays, [1] rays whose hit rank differs, [2] rays with the same
+// rank but a different t, [3] rays where B misses but A hits, [4] rays where A misses but B hits.
+struct CompareParams {
+    RenderParams A;
+    const float4* __restrict__ nodes_b;
+    const float4* __restrict__ prims_b;
+    int n_nodes_b, n_layouts_b;
+    int width_a, width_b;
+};
+
+__global__ __launch_bounds__(256) void crt_compare_kernel(CompareParams Q) {
+    const RenderParams& P = Q.A;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    if (x >= P.width || y >= P.height) return;
+    const int pix = y * P.width + x;
+    PathState S;
+    const uint32_t* r = P.rng + 6 * (size_t)pix;
+    S.s = Rng{r[0], r[1], r[2], r[3], r[4], r[5]};
+    S.pixel = v3(0.f, 0.f, 0.f);
+    S.o = v3(0, 0, 0); S.d = v3(0, 0, 1); S.thr = v3(1, 1, 1);
+    S.remaining = P.spp; S.bounce = 0; S.need_new = true; S.rays = 0; S.paths = 0;
+    const crt_camera_desc& Cd = P.cam;
+    CamRegs C;
+    C.pos = v3(Cd.origin[0], Cd.origin[1], Cd.origin[2]);
+    C.llc = v3(Cd.lower_left[0], Cd.lower_left[1], Cd.lower_left[2]);
+    C.hor = v3(Cd.horizontal[0], Cd.horizontal[1], Cd.horizontal[2]);
+    C.ver = v3(Cd.vertical[0], Cd.vertical[1], Cd.vertical[2]);
+    C.right = v3(Cd.right[0], Cd.right[1], Cd.right[2]);
+    C.up = v3(Cd.up[0], Cd.up[1], Cd.up[2]);
+    C.lens = Cd.lens_radius;
+    C.fw = (float)P.width;
+    C.fh = (float)P.height;
+    TraceCounts cnt{0, 0, 0, 0, 0, 0};
+    unsigned long long n_rank = 0, n_t = 0, n_bmiss = 0, n_amiss = 0;
+    while (next_ray(S, C, x, y, P.max_bounces)) {
+        ++S.rays;
+        float ta, tb;
+        const int ha = Q.width_a == 4 ? trace4(P.nodes, P.prims, S.o, S.d, ta)
+                                      : trace<false>(P.nodes, P.prims, P.n_nodes, layout_base(S.d, P.n_layouts, P.n_nodes),
+                                                     S.o, S.d, ta, cnt);
+        const int hb = Q.width_b == 4 ? trace4(Q.nodes_b, Q.prims_b, S.o, S.d, tb)
+                                      : trace<false>(Q.nodes_b, Q.prims_b, Q.n_nodes_b,
+                                                     layout_base(S.d, Q.n_layouts_b, Q.n_nodes_b), S.o, S.d, tb, cnt);
+        if (ha != hb) {
+            ++n_rank;
+            n_bmiss += (hb < 0);
+            n_amiss += (ha < 0);
+        } else if (ha >= 0 && __float_as_uint(ta) != __float_as_uint(tb)) {
+            ++n_t;
+        }
+        shade(S, P, ha, ta);
+    }
+    atomicAdd(&P.counters[0], (unsigned long long)S.rays);
+    if (n_rank) atomicAdd(&P.counters[1], n_rank);
+    if (n_t) atomicAdd(&P.counters[2], n_t);
+    if (n_bmiss) atomicAdd(&P.counters[3], n_bmiss);
+    if (n_amiss) atomicAdd(&P.counters[4], n_amiss);
 }
 
 // curand_init(seed, subsequence_base + pixel, 0) (CUDAKernels.h:18-26): scrambled seed, then
@@ -826,12 +1186,44 @@ const std::vector<uint32_t>& seq_tables() {
 
 inline float i2f(int v) { float f; std::memcpy(&f, &v, 4); return f; }
 
+inline bool zero_thickness(const float bmin[3], const float bmax[3]) {
+    // AABB::hit can never report such a box (the slab of that axis is empty: tmax <= tmin)
+    return bmin[0] == bmax[0] || bmin[1] == bmax[1] || bmin[2] == bmax[2];
+}
+
+// Flattens the reference's scene + mesh BVHs into the threaded layout and records, per primitive,
+// its reference DFS rank (the order BVHNode::hit / Mesh::hit visit primitives) and whether any box
+// on its path is zero-thickness (then the reference never reports it).
 struct Flattener {
     const crt_scene_desc* D;
     std::vector<float4> nodes, prims;
     std::vector<int> mesh_prim_base;
+    std::vector<int> rank_of;        // per prim
+    std::vector<char> reachable;     // per prim
+    std::vector<int> rank_code;      // per rank: prim code
     int max_depth = 0;
     std::string err;
+
+    void visit_prim(int p, int code, bool thin) {
+        if (rank_of[p] >= 0) return;
+        rank_of[p] = (int)rank_code.size();
+        rank_code.push_back(code);
+        reachable[p] = !thin;
+    }
+    // Primitives no leaf references get the remaining ranks (never hit); ranks go into the records.
+    void finalize_ranks() {
+        const int n = (int)(prims.size() / 3);
+        for (int p = 0; p < n; ++p) {
+            if (rank_of[p] < 0) {
+                rank_of[p] = (int)rank_code.size();
+                rank_code.push_back(p);
+                reachable[p] = 0;
+            }
+            const bool sphere = (rank_code[rank_of[p]] & SPHERE_BIT) != 0;
+            if (sphere) prims[3 * p + 1].z = i2f(rank_of[p]);
+            prims[3 * p + 2].z = i2f(rank_of[p]);
+        }
+    }
 
     int push_node(const float bmin[3], const float bmax[3], int a, int b) {
         nodes.push_back(make_float4(bmin[0], bmin[1], bmin[2], bmax[0]));
@@ -841,15 +1233,16 @@ struct Flattener {
     void set_a(int idx, int a) { nodes[2 * idx + 1].z = i2f(a); }
     int count() const { return (int)(nodes.size() / 2); }
 
-    bool emit_mesh(int m, int ni, int depth) {
+    bool emit_mesh(int m, int ni, int depth, bool thin) {
         const crt_mesh_desc& M = D->meshes[m];
         if (ni < 0 || ni >= M.node_count) { err = "mesh node index out of range"; return false; }
         if (depth > 4096) { err = "mesh BVH too deep"; return false; }
         max_depth = std::max(max_depth, depth);
         const crt_bvh_node_desc& N = M.nodes[ni];
+        thin = thin || zero_thickness(N.bmin, N.bmax);
         if (!N.is_leaf) {
             int idx = push_node(N.bmin, N.bmax, 0, NODE_MESH_INNER);
-            if (!emit_mesh(m, N.left, depth + 1) || !emit_mesh(m, N.right, depth + 1)) return false;
+            if (!emit_mesh(m, N.left, depth + 1, thin) || !emit_mesh(m, N.right, depth + 1, thin)) return false;
             set_a(idx, count());
         } else {
             if (N.obj_index < 0 || N.obj_count < 0 || N.obj_index % 3 || N.obj_count % 3 ||
@@ -857,17 +1250,19 @@ struct Flattener {
             long first = mesh_prim_base[m] + N.obj_index / 3;
             if (first >= SPHERE_BIT) { err = "too many primitives"; return false; }
             push_node(N.bmin, N.bmax, N.obj_count / 3, (int)first);
+            for (int k = 0; k < (int)N.obj_count / 3; ++k) visit_prim((int)first + k, (int)first + k, thin);
         }
         return true;
     }
-    bool emit_scene(int ni, int depth) {
+    bool emit_scene(int ni, int depth, bool thin) {
         if (ni < 0 || ni >= D->n_scene_nodes) { err = "scene node index out of range"; return false; }
         if (depth > 4096) { err = "scene BVH too deep"; return false; }
         max_depth = std::max(max_depth, depth);
         const crt_bvh_node_desc& N = D->scene_nodes[ni];
+        thin = thin || zero_thickness(N.bmin, N.bmax);
         if (!N.is_leaf) {
             int idx = push_node(N.bmin, N.bmax, 0, NODE_SCENE_INNER);
-            if (!emit_scene(N.left, depth + 1) || !emit_scene(N.right, depth + 1)) return false;
+            if (!emit_scene(N.left, depth + 1, thin) || !emit_scene(N.right, depth + 1, thin)) return false;
             set_a(idx, count());
             return true;
         }
@@ -876,7 +1271,7 @@ struct Flattener {
         if (O.kind == CRT_OBJECT_MESH) {
             if (O.index < 0 || O.index >= D->n_meshes) { err = "mesh object index out of range"; return false; }
             int idx = push_node(N.bmin, N.bmax, 0, NODE_SCENE_INNER);
-            if (D->meshes[O.index].node_count > 0 && !emit_mesh(O.index, 0, depth + 1)) return false;
+            if (D->meshes[O.index].node_count > 0 && !emit_mesh(O.index, 0, depth + 1, thin)) return false;
             set_a(idx, count());
         } else if (O.kind == CRT_OBJECT_SPHERE) {
             if (O.index < 0 || O.index >= D->n_spheres) { err = "sphere object index out of range"; return false; }
@@ -885,7 +1280,10 @@ struct Flattener {
             if (p >= SPHERE_BIT) { err = "too many primitives"; return false; }
             prims.push_back(make_float4(S.center[0], S.center[1], S.center[2], S.radius));
             prims.push_back(make_float4(S.radius * S.radius, i2f(S.material), 0.f, 0.f));   // Sphere.cuh:21
-            prims.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+            prims.push_back(make_float4(0.f, i2f(S.material), 0.f, i2f(1)));                  // word 11 = 1: sphere
+            rank_of.push_back(-1);
+            reachable.push_back(0);
+            visit_prim(p, SPHERE_BIT | p, thin);
             push_node(N.bmin, N.bmax, 0, SPHERE_BIT | p);
         } else {
             err = "unknown object kind";
@@ -921,7 +1319,165 @@ struct Flattener {
                 prims.push_back(make_float4(e2[2], i2f((int)mat), 0.f, 0.f));
             }
         }
+        rank_of.assign(prims.size() / 3, -1);
+        reachable.assign(prims.size() / 3, 0);
         return true;
+    }
+};
+
+// CRT_BVH_REBUILT: binned-SAH tree over the reachable primitives of a flattened reference scene,
+// emitted as `layouts` threaded arrays (crt_sah.h).  Primitive records keep their rank.
+struct Rebuilt {
+    std::vector<float4> nodes, prims;
+    std::vector<int> rank_code;
+    int n_nodes = 0, max_depth = 0;
+    long excluded = 0;
+    std::string err;
+
+    int width = 2;
+    int stack_bound = 0;   // width 4: most stack entries any traversal can hold
+
+    bool build(const Flattener& F, int leaf_size, int layouts, float trav_cost, int wide) {
+        width = wide;
+        const int n = (int)(F.prims.size() / 3);
+        std::vector<crt_sah::Item> items;
+        items.reserve(n);
+        for (int p = 0; p < n; ++p) {
+            const bool sphere = (F.rank_code[F.rank_of[p]] & SPHERE_BIT) != 0;
+            if (!F.reachable[p]) { excluded += !sphere; continue; }
+            const float4 f0 = F.prims[3 * p], f1 = F.prims[3 * p + 1], f2 = F.prims[3 * p + 2];
+            crt_sah::Item it;
+            it.src = p;
+            it.sphere = sphere;
+            if (sphere) {
+                const float c[3] = {f0.x, f0.y, f0.z}, r = std::fabs(f0.w);
+                for (int a = 0; a < 3; ++a) { it.lo[a] = c[a] - r; it.hi[a] = c[a] + r; }
+            } else {
+                const float v0[3] = {f0.x, f0.y, f0.z};
+                const float e1[3] = {f0.w, f1.x, f1.y}, e2[3] = {f1.z, f1.w, f2.x};
+                for (int a = 0; a < 3; ++a) {
+                    const float v1 = v0[a] + e1[a], v2 = v0[a] + e2[a];
+                    it.lo[a] = std::min(v0[a], std::min(v1, v2));
+                    it.hi[a] = std::max(v0[a], std::max(v1, v2));
+                }
+            }
+            bool finite = true;
+            for (int a = 0; a < 3; ++a) {
+                it.c[a] = 0.5f * it.lo[a] + 0.5f * it.hi[a];
+                finite = finite && std::isfinite(it.lo[a]) && std::isfinite(it.hi[a]);
+            }
+            if (!finite) { err = "non-finite primitive bounds"; return false; }
+            items.push_back(it);
+        }
+        rank_code.assign(F.rank_code.size(), 0);
+        if (items.empty()) {   // nothing hittable: one empty-box node that no ray enters
+            const float lo[3] = {0, 0, 0};
+            prims.assign(3, make_float4(0, 0, 0, 0));
+            for (int l = 0; l < layouts; ++l) {
+                nodes.push_back(make_float4(lo[0], lo[1], lo[2], lo[0]));
+                nodes.push_back(make_float4(lo[1], lo[2], i2f(1), i2f(NODE_MESH_INNER)));
+            }
+            n_nodes = 1;
+            return true;
+        }
+        crt_sah::Builder B(std::move(items), leaf_size, trav_cost);
+        B.build();
+        max_depth = B.max_depth();
+        const auto& its = B.items();
+        if (width == 4) return emit4(F, B.nodes(), its);
+        prims.resize(3 * its.size());
+        for (size_t i = 0; i < its.size(); ++i) {
+            const int p = its[i].src;
+            for (int q = 0; q < 3; ++q) prims[3 * i + q] = F.prims[3 * p + q];
+            rank_code[F.rank_of[p]] = its[i].sphere ? (SPHERE_BIT | (int)i) : (int)i;
+        }
+        const auto& bn = B.nodes();
+        n_nodes = (int)bn.size();
+        nodes.reserve(2 * (size_t)n_nodes * layouts);
+        for (int l = 0; l < layouts; ++l) {
+            const size_t base = nodes.size() / 2;
+            emit(bn, its, 0, l, layouts, base);
+        }
+        return true;
+    }
+
+private:
+    // 4-wide nodes in BFS order (internal children of a node consecutive), primitives re-laid out so the
+    // leaf children of every node are consecutive in slot order.  See the node format at wide_boxes().
+    bool emit4(const Flattener& F, const std::vector<crt_sah::Node>& bn, const std::vector<crt_sah::Item>& its) {
+        std::vector<int> queue{0};
+        std::vector<crt_sah::Wide> wide;
+        prims.clear();
+        for (size_t qi = 0; qi < queue.size(); ++qi) {
+            const crt_sah::Wide w = crt_sah::open_children(bn, queue[qi]);
+            wide.push_back(w);
+            const int first_child = (int)queue.size();
+            for (int s = 0; s < w.n_internal; ++s) queue.push_back(w.bin[s]);
+            const int leaf_first = (int)(prims.size() / 3);
+            uint32_t counts = 0;
+            for (int s = w.n_internal; s < w.n_slots; ++s) {
+                const crt_sah::Node& L = bn[w.bin[s]];
+                if (L.count > 255) { err = "leaf too large"; return false; }
+                counts |= (uint32_t)L.count << (8 * s);
+                for (int i = L.first; i < L.first + L.count; ++i) {
+                    const int src = its[i].src, np = (int)(prims.size() / 3);
+                    for (int q = 0; q < 3; ++q) prims.push_back(F.prims[3 * src + q]);
+                    rank_code[F.rank_of[src]] = its[i].sphere ? (SPHERE_BIT | np) : np;
+                }
+            }
+            if (prims.size() / 3 >= (size_t)SPHERE_BIT) { err = "too many primitives"; return false; }
+            float row[6][4];
+            for (int s = 0; s < 4; ++s) {
+                for (int a = 0; a < 3; ++a) {
+                    float lo = 1e30f, hi = 1e30f;   // empty slot: zero-thickness, never hit
+                    if (s < w.n_slots) { lo = bn[w.bin[s]].lo[a]; hi = bn[w.bin[s]].hi[a]; }
+                    row[2 * a][s] = lo;
+                    row[2 * a + 1][s] = hi;
+                }
+            }
+            for (int r = 0; r < 6; ++r) nodes.push_back(make_float4(row[r][0], row[r][1], row[r][2], row[r][3]));
+            nodes.push_back(make_float4(i2f(first_child), i2f(w.n_internal | (w.n_slots << 8)), i2f(leaf_first),
+                                        i2f((int)counts)));
+            nodes.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+        }
+        n_nodes = (int)queue.size();
+        // stack bound: visiting a node pushes (hit internal children - 1); children are visited later
+        std::vector<int> bound(n_nodes, 0);
+        for (int n = n_nodes - 1; n >= 0; --n) {
+            const int fc = i2i(nodes[8 * (size_t)n + 6].x), m = wide[n].n_internal;
+            int b = 0;
+            for (int s = 0; s < m; ++s) b = std::max(b, bound[fc + s]);
+            bound[n] = m > 0 ? b + m - 1 : 0;
+        }
+        stack_bound = bound[0] + 1;
+        return true;
+    }
+    static int i2i(float f) { int v; std::memcpy(&v, &f, 4); return v; }
+
+    void emit(const std::vector<crt_sah::Node>& bn, const std::vector<crt_sah::Item>& its, int ni, int layout,
+              int layouts, size_t base) {
+        const crt_sah::Node& N = bn[ni];
+        const size_t idx = nodes.size() / 2;
+        int a = 0, b;
+        if (N.child[0] < 0) {
+            if (its[N.first].sphere) b = SPHERE_BIT | N.first;
+            else { a = N.count; b = N.first; }
+        } else {
+            b = NODE_MESH_INNER;
+        }
+        nodes.push_back(make_float4(N.lo[0], N.lo[1], N.lo[2], N.hi[0]));
+        nodes.push_back(make_float4(N.hi[1], N.hi[2], i2f(a), i2f(b)));
+        if (N.child[0] < 0) return;
+        int first = N.child[0], second = N.child[1];
+        if (layouts == 6) {   // near child first along the layout's direction
+            const int ax = layout / 2;
+            const bool neg = layout & 1;
+            const float c0 = bn[first].lo[ax] + bn[first].hi[ax], c1 = bn[second].lo[ax] + bn[second].hi[ax];
+            if (neg ? (c1 > c0) : (c1 < c0)) std::swap(first, second);
+        }
+        emit(bn, its, first, layout, layouts, base);
+        emit(bn, its, second, layout, layouts, base);
+        nodes[2 * idx + 1].z = i2f((int)(nodes.size() / 2 - base));   // skip, relative to the layout
     }
 };
 
@@ -932,8 +1488,13 @@ struct crt_scene {
     float4* d_nodes = nullptr;
     float4* d_prims = nullptr;
     float4* d_mats = nullptr;
-    int n_nodes = 0, n_prims = 0, n_mats = 0;
+    int* d_rank_code = nullptr;
+    int n_nodes = 0, n_prims = 0, n_mats = 0, n_ranks = 0;   // n_nodes per layout
     int max_depth = 0;
+    int bvh = CRT_BVH_REFERENCE, layouts = 1;
+    int width = 2;                 // 2: threaded layouts (variants 0-3); 4: 4-wide nodes (variant 4)
+    int stack_cap = 0;             // width 4: traversal-stack entries a ray can need
+    long excluded = 0;
 };
 
 struct crt_renderer {
@@ -952,6 +1513,9 @@ struct crt_renderer {
     unsigned long long diag[3] = {0, 0, 0};
     int regen_threshold = 24;
     int min_waves = 5;             // variant 2 occupancy target: 1 (compiler's choice), 5, 6 or 8
+    uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
+    size_t ovf_entries = 0;
+    int stack_lds = STACK_LDS;     // variant 4: per-lane stack entries kept in LDS
 };
 
 namespace {
@@ -979,12 +1543,74 @@ int crt_device_count(int* out) {
 }
 
 int crt_scene_create(const crt_scene_desc* D, int device, crt_scene** out) {
-    if (!D || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
-    *out = nullptr;
+    return crt_scene_create_ex(D, device, nullptr, out);
+}
+
+}  // extern "C"
+
+// Host half of scene creation: flatten the reference BVHs (ranks, reachability) and, for CRT_BVH_REBUILT,
+// build the SAH tree.  Shared by crt_scene_create_ex and crt_scene_export.
+static int build_scene_arrays(const crt_scene_desc* D, const crt_scene_options* opts, crt_scene_options& o,
+                              Flattener& F, Rebuilt& RB) {
+    o = crt_scene_options{};
+    if (opts) o = *opts;
+    if (o.bvh != CRT_BVH_REFERENCE && o.bvh != CRT_BVH_REBUILT) return set_error(CRT_ERR_INVALID_ARGUMENT, "unknown bvh mode");
+    if (o.leaf_size == 0) o.leaf_size = 4;
+    if (o.layouts == 0) o.layouts = 6;
+    if (o.traversal_cost == 0.f) o.traversal_cost = 1.f;
+    if (o.width == 0) o.width = 4;
+    if (o.width != 2 && o.width != 4) return set_error(CRT_ERR_INVALID_ARGUMENT, "width must be 2 or 4");
+    if (!(o.traversal_cost > 0.f && o.traversal_cost <= 64.f)) return set_error(CRT_ERR_INVALID_ARGUMENT, "traversal_cost must be in (0, 64]");
+    if (o.leaf_size < 1 || o.leaf_size > 16) return set_error(CRT_ERR_INVALID_ARGUMENT, "leaf_size must be 1..16");
+    if (o.layouts != 1 && o.layouts != 6) return set_error(CRT_ERR_INVALID_ARGUMENT, "layouts must be 1 or 6");
     if (D->n_scene_nodes <= 0 || !D->scene_nodes) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene has no BVH nodes");
     if (D->n_materials < 0 || (D->n_materials > 0 && !D->materials)) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad materials");
+    if (!F.build_triangles() || !F.emit_scene(0, 0, false)) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene: " + F.err);
+    F.finalize_ranks();
+    if (o.bvh == CRT_BVH_REBUILT) {
+        if (o.width == 4) o.layouts = 1;
+        if (!RB.build(F, o.leaf_size, o.layouts, o.traversal_cost, o.width)) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene: " + RB.err);
+        if ((size_t)RB.n_nodes * o.layouts * (o.width == 4 ? 8 : 2) >= (size_t)1 << 31)
+            return set_error(CRT_ERR_INVALID_ARGUMENT, "scene too large");
+    }
+    return CRT_OK;
+}
+
+extern "C" {
+
+int crt_scene_export(const crt_scene_desc* D, const crt_scene_options* opts, float* nodes, float* prims,
+                     int32_t* rank_code, int64_t info[8]) {
+    if (!D || !info) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    crt_scene_options o;
     Flattener F{D};
-    if (!F.build_triangles() || !F.emit_scene(0, 0)) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene: " + F.err);
+    Rebuilt RB;
+    if (int rc = build_scene_arrays(D, opts, o, F, RB)) return rc;
+    const bool rebuilt = o.bvh == CRT_BVH_REBUILT;
+    const std::vector<float4>& N = rebuilt ? RB.nodes : F.nodes;
+    const std::vector<float4>& Pr = rebuilt ? RB.prims : F.prims;
+    const std::vector<int>& rc = rebuilt ? RB.rank_code : F.rank_code;
+    info[0] = (int64_t)N.size();
+    info[1] = (int64_t)Pr.size();
+    info[2] = (int64_t)rc.size();
+    info[3] = rebuilt ? RB.n_nodes : F.count();
+    info[4] = rebuilt ? o.layouts : 1;
+    info[5] = rebuilt ? RB.width : 2;
+    info[6] = rebuilt ? RB.stack_bound : 0;
+    info[7] = rebuilt ? RB.excluded : 0;
+    if (nodes) std::memcpy(nodes, N.data(), N.size() * sizeof(float4));
+    if (prims) std::memcpy(prims, Pr.data(), Pr.size() * sizeof(float4));
+    if (rank_code) std::memcpy(rank_code, rc.data(), rc.size() * sizeof(int));
+    return CRT_OK;
+}
+
+int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_options* opts, crt_scene** out) {
+    if (!D || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    crt_scene_options o;
+    Flattener F{D};
+    Rebuilt RB;
+    if (int rc = build_scene_arrays(D, opts, o, F, RB)) return rc;
+    const bool rebuilt = o.bvh == CRT_BVH_REBUILT;
     std::vector<float4> mats;
     for (int i = 0; i < D->n_materials; ++i) {
         const crt_material_desc& M = D->materials[i];
@@ -996,10 +1622,16 @@ int crt_scene_create(const crt_scene_desc* D, int device, crt_scene** out) {
     crt_scene* S = new (std::nothrow) crt_scene;
     if (!S) return set_error(CRT_ERR_OUT_OF_MEMORY, "host allocation failed");
     S->device = device;
-    S->n_nodes = F.count();
-    S->n_prims = (int)(F.prims.size() / 3);
+    S->bvh = o.bvh;
+    S->layouts = rebuilt ? o.layouts : 1;
+    S->n_nodes = rebuilt ? RB.n_nodes : F.count();
+    S->n_prims = (int)((rebuilt ? RB.prims : F.prims).size() / 3);
+    S->n_ranks = (int)F.rank_code.size();
     S->n_mats = D->n_materials;
-    S->max_depth = F.max_depth;
+    S->max_depth = rebuilt ? RB.max_depth : F.max_depth;
+    S->excluded = rebuilt ? RB.excluded : 0;
+    S->width = rebuilt ? RB.width : 2;
+    S->stack_cap = rebuilt ? RB.stack_bound : 0;
     auto up = [&](float4** dst, const std::vector<float4>& src) -> hipError_t {
         size_t bytes = std::max<size_t>(src.size(), 1) * sizeof(float4);
         hipError_t e = hipMalloc((void**)dst, bytes);
@@ -1007,9 +1639,13 @@ int crt_scene_create(const crt_scene_desc* D, int device, crt_scene** out) {
         if (!src.empty()) e = hipMemcpy(*dst, src.data(), src.size() * sizeof(float4), hipMemcpyHostToDevice);
         return e;
     };
+    const std::vector<int>& rc = rebuilt ? RB.rank_code : F.rank_code;
     hipError_t e;
-    if ((e = up(&S->d_nodes, F.nodes)) != hipSuccess || (e = up(&S->d_prims, F.prims)) != hipSuccess ||
-        (e = up(&S->d_mats, mats)) != hipSuccess) {
+    if ((e = up(&S->d_nodes, rebuilt ? RB.nodes : F.nodes)) != hipSuccess ||
+        (e = up(&S->d_prims, rebuilt ? RB.prims : F.prims)) != hipSuccess ||
+        (e = up(&S->d_mats, mats)) != hipSuccess ||
+        (e = hipMalloc((void**)&S->d_rank_code, std::max<size_t>(rc.size(), 1) * sizeof(int))) != hipSuccess ||
+        (!rc.empty() && (e = hipMemcpy(S->d_rank_code, rc.data(), rc.size() * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)) {
         crt_scene_destroy(S);
         return set_error(CRT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e));
     }
@@ -1019,11 +1655,17 @@ int crt_scene_create(const crt_scene_desc* D, int device, crt_scene** out) {
 
 int crt_scene_get_stats(const crt_scene* S, crt_scene_stats* out) {
     if (!S || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
-    out->device_nodes = S->n_nodes;
+    out->device_nodes = (int64_t)S->n_nodes * S->layouts;
+    out->width = S->width;
+    out->stack_bound = S->stack_cap;
     out->device_prims = S->n_prims;
-    out->device_bytes = (int64_t)S->n_nodes * 32 + (int64_t)S->n_prims * 48 + (int64_t)S->n_mats * 48;
+    out->device_bytes = (int64_t)S->n_nodes * S->layouts * (S->width == 4 ? 128 : 32) + (int64_t)S->n_prims * 48 + (int64_t)S->n_mats * 48 +
+                        (int64_t)S->n_ranks * 4;
     out->max_depth = S->max_depth;
     out->n_materials = S->n_mats;
+    out->bvh = S->bvh;
+    out->layouts = S->layouts;
+    out->excluded_prims = S->excluded;
     return CRT_OK;
 }
 
@@ -1033,6 +1675,7 @@ void crt_scene_destroy(crt_scene* S) {
     if (S->d_nodes) (void)hipFree(S->d_nodes);
     if (S->d_prims) (void)hipFree(S->d_prims);
     if (S->d_mats) (void)hipFree(S->d_mats);
+    if (S->d_rank_code) (void)hipFree(S->d_rank_code);
     delete S;
 }
 
@@ -1086,6 +1729,7 @@ void crt_renderer_destroy(crt_renderer* R) {
     if (R->d_rgba) (void)hipFree(R->d_rgba);
     if (R->d_seq) (void)hipFree(R->d_seq);
     if (R->d_counters) (void)hipFree(R->d_counters);
+    if (R->d_ovf) (void)hipFree(R->d_ovf);
     if (R->ev0) (void)hipEventDestroy(R->ev0);
     if (R->ev1) (void)hipEventDestroy(R->ev1);
     delete R;
@@ -1113,6 +1757,12 @@ int crt_renderer_set_occupancy_target(crt_renderer* R, int waves_per_simd) {
     return CRT_OK;
 }
 
+int crt_renderer_set_stack_lds(crt_renderer* R, int entries) {
+    if (!R || entries < 1 || entries > STACK_LDS) return set_error(CRT_ERR_INVALID_ARGUMENT, "stack LDS entries 1..16");
+    R->stack_lds = entries;
+    return CRT_OK;
+}
+
 int crt_renderer_set_regen_threshold(crt_renderer* R, int lanes) {
     if (!R || lanes < 1 || lanes > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "threshold must be 1..64");
     R->regen_threshold = lanes;
@@ -1135,12 +1785,27 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     hipStream_t st = (hipStream_t)stream;
     HIP_TRY(hipMemsetAsync(R->d_counters, 0, 8 * sizeof(unsigned long long), st));
     RenderParams P;
-    P.nodes = S->d_nodes; P.prims = S->d_prims; P.mats = S->d_mats;
-    P.n_nodes = S->n_nodes; P.n_mats = S->n_mats; P.n_prims = S->n_prims;
+    P.nodes = S->d_nodes; P.prims = S->d_prims; P.mats = S->d_mats; P.rank_code = S->d_rank_code;
+    P.n_nodes = S->n_nodes; P.n_mats = S->n_mats; P.n_prims = S->n_prims; P.n_layouts = S->layouts;
     P.err = reinterpret_cast<unsigned*>(R->d_counters + 7);
     P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
     P.accumulate = (flags & CRT_RENDER_ACCUMULATE) ? 1 : 0;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
+    P.ovf = nullptr;
+    P.stack_cap = S->stack_cap;
+    P.stack_lds = R->stack_lds;
+    if (S->width == 4 && S->stack_cap > R->stack_lds) {
+        const size_t need = (size_t)(S->stack_cap - R->stack_lds);
+        if (need > R->ovf_entries) {         // grow the overflow stack region (rarely needed)
+            HIP_TRY(hipStreamSynchronize(st));
+            if (R->d_ovf) (void)hipFree(R->d_ovf);
+            R->d_ovf = nullptr;
+            R->ovf_entries = 0;
+            HIP_TRY(hipMalloc((void**)&R->d_ovf, need * R->width * R->height * 4));
+            R->ovf_entries = need;
+        }
+        P.ovf = R->d_ovf;
+    }
     dim3 grid((R->width + 15) / 16, (R->height + 15) / 16), block(256);
     HIP_TRY(hipEventRecord(R->ev0, st));
     const bool cnt = (flags & CRT_RENDER_COUNT_WORK) != 0;
@@ -1150,7 +1815,12 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, V, W>), grid, block, 0, st, P);  \
         else hipLaunchKernelGGL((crt_render_kernel<false, V, W>), grid, block, 0, st, P);     \
     } while (0)
-    if (R->variant == 0) CRT_LAUNCH(0, 1);
+    if (S->width == 4) {
+        if (R->min_waves >= 5) CRT_LAUNCH(4, 5);
+        else if (R->min_waves >= 4) CRT_LAUNCH(4, 4);
+        else CRT_LAUNCH(4, 1);
+    }
+    else if (R->variant == 0) CRT_LAUNCH(0, 1);
     else if (R->variant == 1) CRT_LAUNCH(1, 1);
     else if (R->variant == 3) {
         if (R->min_waves >= 5) CRT_LAUNCH(3, 5);
@@ -1165,6 +1835,36 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(R->ev1, st));
     R->timed = true;
+    return CRT_OK;
+}
+
+int crt_scene_compare(crt_renderer* R, const crt_scene* A, const crt_scene* B, int spp, int max_bounces,
+                      uint64_t out[5]) {
+    if (!R || !A || !B || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    if (!R->has_camera) return set_error(CRT_ERR_INVALID_ARGUMENT, "camera not set");
+    if (A->device != R->device || B->device != R->device)
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "scenes and renderer on different devices");
+    if (A->n_ranks != B->n_ranks) return set_error(CRT_ERR_INVALID_ARGUMENT, "scenes hold different primitive sets");
+    if (spp < 0 || max_bounces < 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "negative spp / bounces");
+    HIP_TRY(hipSetDevice(R->device));
+    HIP_TRY(hipMemset(R->d_counters, 0, 8 * sizeof(unsigned long long)));
+    CompareParams Q;
+    RenderParams& P = Q.A;
+    P.nodes = A->d_nodes; P.prims = A->d_prims; P.mats = A->d_mats; P.rank_code = A->d_rank_code;
+    P.n_nodes = A->n_nodes; P.n_mats = A->n_mats; P.n_prims = A->n_prims; P.n_layouts = A->layouts;
+    P.err = reinterpret_cast<unsigned*>(R->d_counters + 7);
+    P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
+    P.accumulate = 0; P.regen_threshold = 64;
+    P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
+    Q.nodes_b = B->d_nodes; Q.prims_b = B->d_prims; Q.n_nodes_b = B->n_nodes; Q.n_layouts_b = B->layouts;
+    Q.width_a = A->width; Q.width_b = B->width;
+    dim3 grid((R->width + 15) / 16, (R->height + 15) / 16), block(256);
+    hipLaunchKernelGGL(crt_compare_kernel, grid, block, 0, 0, Q);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long h[8];
+    HIP_TRY(hipMemcpy(h, R->d_counters, sizeof h, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 5; ++i) out[i] = h[i];
     return CRT_OK;
 }
 

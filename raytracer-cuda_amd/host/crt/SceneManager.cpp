@@ -35,7 +35,7 @@ void SceneManager::uploadScene() {
         m_Scene = nullptr;
     }
     crt_scene_desc d = sceneDesc();
-    CRT_CHECK(crt_scene_create(&d, m_Device, &m_Scene));
+    CRT_CHECK(crt_scene_create_ex(&d, m_Device, &m_SceneOptions, &m_Scene));
 }
 
 // :100-196

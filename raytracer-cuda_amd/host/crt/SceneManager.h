@@ -41,6 +41,8 @@ public:
 
     // Reference default model list (SceneManager.h:101-103); override before initializeScene.
     void setModelFiles(const std::vector<std::string>& files) { m_ModelFiles = files; }
+    // Acceleration structure of the device scene (default CRT_BVH_REFERENCE, bit-exact); applies at uploadScene.
+    void setSceneOptions(const crt_scene_options& opts) { m_SceneOptions = opts; }
     const std::vector<std::string>& modelFiles() const { return m_ModelFiles; }
 
     // SceneManager::initializeScene (SceneManager.h:77-98).  randState is accepted for API
@@ -90,4 +92,5 @@ private:
     std::vector<crt_object_desc> m_Objects;
     std::vector<crt_bvh_node_desc> m_SceneBVH;
     crt_scene* m_Scene = nullptr;
+    crt_scene_options m_SceneOptions{};
 };

@@ -58,6 +58,14 @@ int crth_scene_upload(const crth_scene* s, int device, crt_scene** out) {
     return rc;
 }
 
+int crth_scene_upload_ex(const crth_scene* s, int device, const crt_scene_options* opts, crt_scene** out) {
+    if (!s || !out) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    crt_scene_desc d = s->sm.sceneDesc();
+    int rc = crt_scene_create_ex(&d, device, opts, out);
+    if (rc) g_err = crt_last_error();
+    return rc;
+}
+
 int crth_scene_counts(const crth_scene* s, int64_t* c) {
     if (!s || !c) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
     c[0] = (int64_t)s->sm.meshes().size();

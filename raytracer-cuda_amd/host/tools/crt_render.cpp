@@ -2,7 +2,8 @@
 // build the scene with SceneManager, set the camera, render one frame with CUDARenderer and
 // write it as a binary PPM (rows flipped like WindowManager::drawFrame's flipVertically).
 //
-//   crt_render [-w W] [-h H] [-spp N] [-seed S] [-o out.ppm] [-pos x y z] [-fov deg] model.obj...
+//   crt_render [-w W] [-h H] [-spp N] [-seed S] [-o out.ppm] [-pos x y z] [-fov deg] [-bvh reference|rebuilt]
+//              [-leaf N] model.obj...
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -23,6 +24,7 @@ int main(int argc, char** argv) {
         float pos[3] = {0.f, 0.f, 0.3f};
         std::string out = "frame.ppm";
         std::vector<std::string> files;
+        crt_scene_options opts{};
         for (int i = 1; i < argc; ++i) {
             std::string a = argv[i];
             auto need = [&](int k) { if (i + k >= argc) { std::fprintf(stderr, "missing value for %s\n", a.c_str()); std::exit(2); } };
@@ -33,6 +35,8 @@ int main(int argc, char** argv) {
             else if (a == "-o") { need(1); out = argv[++i]; }
             else if (a == "-fov") { need(1); fov = (float)std::atof(argv[++i]); }
             else if (a == "-pos") { need(3); for (float& p : pos) p = (float)std::atof(argv[++i]); }
+            else if (a == "-bvh") { need(1); std::string m = argv[++i]; opts.bvh = m == "rebuilt" ? CRT_BVH_REBUILT : CRT_BVH_REFERENCE; }
+            else if (a == "-leaf") { need(1); opts.leaf_size = std::atoi(argv[++i]); }
             else files.push_back(a);
         }
         const float ASPECT_RATIO = 16.0f / 9.0f;                 // EntryPoint.cu:16-20
@@ -45,6 +49,7 @@ int main(int argc, char** argv) {
         auto config = CUDAHelpers::createRenderConfig(W, H);
         SceneManager scene(W, H);
         scene.setModelFiles(files);
+        scene.setSceneOptions(opts);
         CUDARenderer renderer(W, H);
         auto t0 = std::chrono::steady_clock::now();
         renderer.initialize(config, seed);

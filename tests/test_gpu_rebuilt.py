@@ -1,0 +1,139 @@
+"""CRT_BVH_REBUILT on the GPU vs the reference semantics (oracle / reference-BVH device scene).
+
+The rebuilt BVH keeps the reference's hit rule (closest t, ties to the higher reference DFS rank, primitives
+in zero-thickness reference boxes excluded), so almost every ray returns the reference's hit bit for bit.
+It can differ only where the reference's unpadded boxes round away a genuine hit; such a ray changes the
+rest of its pixel's path.  Bar (north star): per-channel RMS of the resolved linear colour <= 1e-4 against
+the oracle, with the per-ray agreement measured by crt_scene_compare (both structures trace the same rays)
+and the fraction of bit-identical pixels bounded from below.
+"""
+import numpy as np
+import pytest
+
+import crt_amd
+
+pytestmark = pytest.mark.gpu
+RMS_TOL = 1e-4
+
+CONFIGS = {"w4": dict(width=4), "w4l8": dict(width=4, leaf_size=8, traversal_cost=2),
+           "w2l16": dict(width=2, leaf_size=16, traversal_cost=6)}
+
+
+@pytest.fixture(scope="module")
+def rebuilt(device_scenes):
+    out = {}
+    for scene in ("cornell", "cornell_bunny"):
+        hs, _ = device_scenes[scene]
+        for k, opts in CONFIGS.items():
+            out[scene, k] = hs.upload(0, bvh="rebuilt", **opts)
+    return out
+
+
+def _frame(dev, w, h, spp, bounces, cam, variant=3, seed=41, stack_lds=16):
+    r = crt_amd.Renderer(w, h)
+    r.set_kernel_variant(variant)
+    r.set_stack_lds(stack_lds)
+    r.set_camera(cam)
+    r.init_rand(seed)
+    r.render(dev, spp, bounces)
+    r.resolve(crt_amd.pixel_sample_scale(spp))
+    r.synchronize()
+    return r
+
+
+def _compare(lin, o_sum, spp, min_equal):
+    rms = np.sqrt(np.mean(((lin - o_sum) / spp).astype(np.float64) ** 2, axis=(0, 1)))
+    assert (rms <= RMS_TOL).all(), f"per-channel RMS {rms}"
+    eq = np.mean(np.all(lin.view(np.uint32) == o_sum.view(np.uint32), axis=-1))
+    assert eq >= min_equal, f"only {eq:.6f} of pixels bit-identical"
+    return rms, eq
+
+
+def test_rebuilt_stats(rebuilt, device_scenes):
+    ref = device_scenes["cornell_bunny"][1].stats()
+    for k, opts in CONFIGS.items():
+        st = rebuilt["cornell_bunny", k].stats()
+        assert st["bvh"] == 1 and st["width"] == opts["width"]
+        assert st["device_prims"] + st["excluded_prims"] == ref["device_prims"]
+        if opts["width"] == 4:
+            assert st["stack_bound"] > 1
+
+
+@pytest.mark.parametrize("cfg", list(CONFIGS))
+@pytest.mark.parametrize("bounces", [4, 20])
+def test_config_a_rebuilt(rebuilt, oracle_scenes, cfg, bounces):
+    """Config A (Cornell, 256x256, 16 spp) rendered through the rebuilt BVH vs the oracle."""
+    w = h = 256
+    spp = 16
+    cam = crt_amd.camera(spp)
+    r = _frame(rebuilt["cornell", cfg], w, h, spp, bounces, cam)
+    o_sum, o_rgba, o_cnt = oracle_scenes["cornell"].render(crt_amd.camera_floats(cam), w, h, spp, bounces)
+    _compare(r.linear(), o_sum, spp, 0.999)
+    assert abs(r.counters()["rays"] - o_cnt["rays"]) <= 1e-4 * o_cnt["rays"]
+
+
+@pytest.mark.parametrize("cfg", list(CONFIGS))
+def test_cornell_bunny_rebuilt(rebuilt, oracle_scenes, cfg):
+    w, h, spp = 128, 72, 32
+    cam = crt_amd.camera(spp)
+    r = _frame(rebuilt["cornell_bunny", cfg], w, h, spp, 20, cam)
+    o_sum, _, _ = oracle_scenes["cornell_bunny"].render(crt_amd.camera_floats(cam), w, h, spp, 20)
+    _compare(r.linear(), o_sum, spp, 0.999)
+    c = r.counters()
+    assert c["rays"] > 0
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_threaded_rebuilt_all_variants_identical(rebuilt, variant):
+    """Width-2 rebuilt layouts run on every threaded variant; all give the same frame bit for bit."""
+    w, h, spp = 96, 54, 8
+    cam = crt_amd.camera(spp)
+    base = _frame(rebuilt["cornell_bunny", "w2l16"], w, h, spp, 20, cam, variant=3).linear()
+    got = _frame(rebuilt["cornell_bunny", "w2l16"], w, h, spp, 20, cam, variant=variant).linear()
+    assert np.array_equal(base.view(np.uint32), got.view(np.uint32))
+
+
+def test_wide_stack_in_hbm_identical(rebuilt):
+    """Variant 4 with 1 LDS stack entry (everything deeper in the HBM overflow region) == 16 entries."""
+    w, h, spp = 160, 90, 8
+    cam = crt_amd.camera(spp)
+    a = _frame(rebuilt["cornell_bunny", "w4"], w, h, spp, 20, cam, stack_lds=16)
+    b = _frame(rebuilt["cornell_bunny", "w4"], w, h, spp, 20, cam, stack_lds=1)
+    assert np.array_equal(a.linear().view(np.uint32), b.linear().view(np.uint32))
+    assert a.counters()["rays"] == b.counters()["rays"]
+
+
+@pytest.mark.parametrize("cfg", list(CONFIGS))
+def test_per_ray_agreement(rebuilt, device_scenes, cfg):
+    """Every ray traced through both structures: hit primitive and t agree except at rounding events."""
+    r = crt_amd.Renderer(640, 360)
+    r.set_camera(crt_amd.camera(4))
+    r.init_rand(41)
+    c = r.compare(device_scenes["cornell_bunny"][1], rebuilt["cornell_bunny", cfg], 4, 20)
+    assert c["rays"] > 2_000_000
+    assert c["t_mismatch"] == 0
+    assert c["rank_mismatch"] <= 1e-6 * c["rays"], c
+
+
+def test_full_size_rebuilt_sampled_pixels(rebuilt, oracle_scenes):
+    """Headline geometry (2560x1440) through the 4-wide kernel at 4 spp: bands vs the oracle, determinism."""
+    w, h, spp = 2560, 1440, 4
+    cam = crt_amd.camera(spp)
+    dev = rebuilt["cornell_bunny", "w4"]
+    r = _frame(dev, w, h, spp, 20, cam)
+    lin = r.linear()
+    r.init_rand(41)
+    r.render(dev, spp, 20)
+    r.synchronize()
+    assert np.array_equal(lin.view(np.uint32), r.linear().view(np.uint32)), "not deterministic"
+    cf = crt_amd.camera_floats(cam)
+    for (x0, y0, x1, y1) in [(0, 0, 64, 4), (1200, 700, 1296, 708), (1700, 900, 1760, 960)]:
+        o_sum, _, _ = oracle_scenes["cornell_bunny"].render(cf, w, h, spp, 20, rect=(x0, y0, x1, y1))
+        _compare(lin[y0:y1, x0:x1], o_sum, spp, 0.99)
+
+
+def test_golden_fixture_rebuilt(rebuilt):
+    from pathlib import Path
+    g = np.load(Path(__file__).resolve().parent / "golden" / "cornell_bunny_64x36_16spp.npz")
+    r = _frame(rebuilt["cornell_bunny", "w4"], 64, 36, 16, 20, crt_amd.camera(16))
+    _compare(r.linear(), g["sum"], 16, 0.99)

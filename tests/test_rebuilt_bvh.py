@@ -1,0 +1,284 @@
+"""CRT_BVH_REBUILT host build, checked on the CPU through crt_scene_export (no GPU needed).
+
+* structure of the 4-wide and threaded binary layouts: every reachable primitive exactly once, rank_code
+  consistent, children consecutive, child boxes enclose their primitives (padded), stack bound;
+* traversal semantics: a float32 restatement of the variant-4 traversal over the exported nodes returns
+  the brute-force closest hit (t, then the higher reference rank) for random rays — i.e. the padded
+  boxes never cull a hit and the rank rule reproduces the reference's tie-breaking.
+"""
+import numpy as np
+import pytest
+
+import crt_amd
+from crt_amd import assets
+
+F32 = np.float32
+
+
+@pytest.fixture(scope="module")
+def host_scene():
+    return crt_amd.HostScene(assets.scene_files("cornell_bunny"))
+
+
+@pytest.fixture(scope="module")
+def ref_export(host_scene):
+    return host_scene.export("reference")
+
+
+def _i(a):
+    return np.asarray(a, np.float32).view(np.int32)
+
+
+def _prim_ranks(prims):
+    return _i(prims.reshape(-1, 3, 4)[:, 2, 2])
+
+
+def _is_sphere(prims):
+    return _i(prims.reshape(-1, 3, 4)[:, 2, 3]) == 1
+
+
+def test_reference_export_ranks(ref_export):
+    e = ref_export
+    assert e["width"] == 2 and e["layouts"] == 1
+    ranks = _prim_ranks(e["prims"])
+    assert sorted(ranks.tolist()) == list(range(e["ranks"]))
+    codes = e["rank_code"]
+    idx = codes & ~(1 << 30)
+    assert np.array_equal(ranks[idx], np.arange(e["ranks"]))
+    assert np.array_equal((codes >> 30) & 1, _is_sphere(e["prims"])[idx].astype(np.int32))
+
+
+@pytest.mark.parametrize("opts", [dict(width=4), dict(width=4, leaf_size=8, traversal_cost=2),
+                                  dict(width=2, leaf_size=16, traversal_cost=6)])
+def test_rebuilt_structure(host_scene, ref_export, opts):
+    e = host_scene.export("rebuilt", **opts)
+    n_ref = ref_export["ranks"]
+    assert e["ranks"] == n_ref
+    prims = e["prims"].reshape(-1, 3, 4)
+    ranks = _prim_ranks(e["prims"])
+    assert len(set(ranks.tolist())) == len(ranks), "a primitive appears twice"
+    assert len(ranks) + e["excluded"] == n_ref
+    codes = e["rank_code"]
+    for p, r in enumerate(ranks):
+        assert codes[r] & ~(1 << 30) == p
+    # reference primitive with the same rank has the same record (apart from nothing)
+    ref_prims = ref_export["prims"].reshape(-1, 3, 4)
+    ref_idx = ref_export["rank_code"][ranks] & ~(1 << 30)
+    assert np.array_equal(prims.view(np.uint32), ref_prims[ref_idx].view(np.uint32))
+    if e["width"] == 4:
+        _check_wide(e, prims)
+    else:
+        _check_threaded(e, prims)
+
+
+def _prim_box(rec):
+    if _i(rec[2, 3]) == 1:
+        c, r = rec[0, :3], abs(rec[0, 3])
+        return c - r, c + r
+    v0 = rec[0, :3]
+    e1 = np.array([rec[0, 3], rec[1, 0], rec[1, 1]], np.float32)
+    e2 = np.array([rec[1, 2], rec[1, 3], rec[2, 0]], np.float32)
+    pts = np.stack([v0, v0 + e1, v0 + e2])
+    return pts.min(0), pts.max(0)
+
+
+def _check_wide(e, prims):
+    nodes = e["nodes"].reshape(-1, 8, 4)
+    n = len(nodes)
+    assert n == e["nodes_per_layout"]
+    seen = np.zeros(len(prims), np.int32)
+    parent_of = {0: None}
+    for i in range(n):
+        q = nodes[i]
+        fc, meta, lf, counts = _i(q[6])
+        n_int, n_slots = meta & 0xFF, meta >> 8
+        assert 0 <= n_int <= n_slots <= 4
+        off = 0
+        for s in range(4):
+            lo = np.array([q[0, s], q[2, s], q[4, s]])
+            hi = np.array([q[1, s], q[3, s], q[5, s]])
+            c = (counts >> (8 * s)) & 0xFF
+            if s >= n_slots:
+                assert (lo == 1e30).all() and (hi == 1e30).all() and c == 0
+            elif s < n_int:
+                assert c == 0
+                child = fc + s
+                assert 0 < child < n and child not in parent_of
+                parent_of[child] = (i, lo, hi)
+            else:
+                assert c > 0
+                for p in range(lf + off, lf + off + c):
+                    seen[p] += 1
+                    plo, phi = _prim_box(prims[p])
+                    assert (plo > lo).all() and (phi < hi).all(), "leaf box must strictly enclose (padding)"
+                off += c
+    assert (seen == 1).all(), "every primitive in exactly one leaf"
+    assert len(parent_of) == n
+    # child node boxes inside their parent's slot box
+    for child, pr in parent_of.items():
+        if pr is None:
+            continue
+        _, lo, hi = pr
+        q = nodes[child]
+        meta = _i(q[6])[1]
+        for s in range(meta >> 8):
+            assert q[0, s] >= lo[0] and q[2, s] >= lo[1] and q[4, s] >= lo[2]
+            assert q[1, s] <= hi[0] and q[3, s] <= hi[1] and q[5, s] <= hi[2]
+    # stack bound = max over root paths of sum(internal children - 1), recomputed independently
+    bound = np.zeros(n, np.int64)
+    for i in range(n - 1, -1, -1):
+        fc, meta = _i(nodes[i, 6])[:2]
+        m = meta & 0xFF
+        bound[i] = (m - 1 + max(bound[fc + s] for s in range(m))) if m else 0
+    assert e["stack_bound"] == bound[0] + 1
+
+
+def _check_threaded(e, prims):
+    nodes = e["nodes"].reshape(e["layouts"], -1, 2, 4)
+    seen = np.zeros(len(prims), np.int32)
+    for lay in range(e["layouts"]):
+        L = nodes[lay]
+        cnt = np.zeros(len(prims), np.int32)
+        for i in range(len(L)):
+            a, b = _i(L[i, 1, 2:])
+            if b == -1:
+                assert i < a <= len(L)
+            elif b >= 1 << 30:
+                cnt[b - (1 << 30)] += 1
+            else:
+                cnt[b:b + a] += 1
+        assert (cnt == 1).all()
+        seen += cnt
+    assert (seen == e["layouts"]).all()
+
+
+# ---------------------------------------------------------------- traversal semantics
+def _mt_all(prims, o, d, tmax):
+    """Möller–Trumbore over all triangle records, float32 with the kernel's operation order."""
+    f0, f1, f2 = prims[:, 0], prims[:, 1], prims[:, 2]
+    v0 = f0[:, :3]
+    e1 = np.stack([f0[:, 3], f1[:, 0], f1[:, 1]], 1)
+    e2 = np.stack([f1[:, 2], f1[:, 3], f2[:, 0]], 1)
+
+    def cross(u, v):
+        return np.stack([u[..., 1] * v[..., 2] - u[..., 2] * v[..., 1], u[..., 2] * v[..., 0] - u[..., 0] * v[..., 2],
+                         u[..., 0] * v[..., 1] - u[..., 1] * v[..., 0]], -1)
+
+    def dot(u, v):
+        return (u[..., 0] * v[..., 0] + u[..., 1] * v[..., 1]) + u[..., 2] * v[..., 2]
+
+    with np.errstate(all="ignore"):
+        dd = np.broadcast_to(d, e2.shape)
+        h = cross(dd, e2)
+        det = dot(e1, h)
+        ok = ~(np.abs(det) < F32(1e-8))
+        f = F32(1) / det
+        s = o - v0
+        u = f * dot(s, h)
+        ok &= ~((u < 0) | (u > 1))
+        q = cross(s, e1)
+        v = f * dot(dd, q)
+        ok &= ~((v < 0) | ((u + v) > 1))
+        t = f * dot(e2, q)
+        ok &= ~((t < F32(0.001)) | (t > tmax))
+    return np.where(ok, t, -1).astype(np.float32)
+
+
+def _sphere_all(prims, o, d, tmax):
+    f0, f1 = prims[:, 0], prims[:, 1]
+    with np.errstate(all="ignore"):
+        oc = o - f0[:, :3]
+        qa = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]
+        hb = (oc[:, 0] * d[0] + oc[:, 1] * d[1]) + oc[:, 2] * d[2]
+        qc = ((oc[:, 0] * oc[:, 0] + oc[:, 1] * oc[:, 1]) + oc[:, 2] * oc[:, 2]) - f1[:, 0]
+        disc = hb * hb - qa * qc
+        sq = np.sqrt(np.maximum(disc, 0)).astype(np.float32)
+        r1 = (-hb - sq) / qa
+        r2 = (-hb + sq) / qa
+        bad1 = (r1 < F32(0.001)) | (r1 > tmax)
+        bad2 = (r2 < F32(0.001)) | (r2 > tmax)
+        t = np.where(bad1, np.where(bad2, -1, r2), r1)
+    return np.where(disc < 0, -1, t).astype(np.float32)
+
+
+def _prim_t(prims, o, d, tmax):
+    sph = _i(prims[:, 2, 3]) == 1
+    t = _mt_all(prims, o, d, tmax)
+    if sph.any():
+        t[sph] = _sphere_all(prims[sph], o, d, tmax)
+    return t
+
+
+def _best(t, ranks, closest=np.float32(np.inf), hit=-1):
+    ok = t >= 0
+    if not ok.any():
+        return closest, hit
+    tm = t[ok].min()
+    r = ranks[ok][t[ok] == tm].max()
+    if tm < closest or (tm == closest and r > hit):
+        return tm, int(r)
+    return closest, hit
+
+
+def _trace_wide(e, prims, ranks, o, d):
+    nodes = e["nodes"].reshape(-1, 8, 4)
+    with np.errstate(all="ignore"):
+        inv = (F32(1) / d).astype(np.float32)
+    closest, hit = np.float32(np.inf), -1
+    stack, node, steps = [], 0, 0
+    while node >= 0:
+        steps += 1
+        q = nodes[node]
+        with np.errstate(all="ignore"):
+            a = [(q[2 * k] - o[k]) * inv[k] for k in range(3)]
+            b = [(q[2 * k + 1] - o[k]) * inv[k] for k in range(3)]
+        t0 = np.fmax(np.fmax(np.fmin(a[0], b[0]), np.fmin(a[1], b[1])), np.fmax(np.fmin(a[2], b[2]), F32(0.001)))
+        t1 = np.fmin(np.fmin(np.fmax(a[0], b[0]), np.fmax(a[1], b[1])), np.fmin(np.fmax(a[2], b[2]), closest))
+        hitm = t0 < t1
+        fc, meta, lf, counts = _i(q[6])
+        n_int = meta & 0xFF
+        entry = closest
+        off = 0
+        for s in range(4):
+            c = (counts >> (8 * s)) & 0xFF
+            if s >= n_int and c and hitm[s]:
+                rng = slice(lf + off, lf + off + c)
+                closest, hit = _best(_prim_t(prims[rng], o, d, entry), ranks[rng], closest, hit)
+            off += c
+        kids = sorted((t0[s], s) for s in range(n_int) if hitm[s])
+        if kids:
+            node = fc + kids[0][1]
+            stack.extend(fc + s for _, s in reversed(kids[1:]))
+        else:
+            node = stack.pop() if stack else -1
+    return closest, hit
+
+
+def test_wide_traversal_equals_brute_force(host_scene):
+    e = host_scene.export("rebuilt", width=4)
+    prims = e["prims"].reshape(-1, 3, 4)
+    ranks = _prim_ranks(e["prims"])
+    rng = np.random.default_rng(5)
+    n_hit = 0
+    for i in range(160):
+        if i % 2:   # aim at the bunny region on the tall box
+            o = rng.uniform([-0.25, 0.0, -0.25], [0.25, 0.5, 0.25]).astype(np.float32)
+            tgt = np.array([-0.096, 0.14, -0.078], np.float32) + rng.normal(0, 0.04, 3).astype(np.float32)
+            d = (tgt - o).astype(np.float32)
+        else:
+            o = rng.uniform([-0.27, 0.01, -0.27], [0.27, 0.54, 0.3]).astype(np.float32)
+            d = rng.normal(size=3).astype(np.float32)
+        brute = _best(_prim_t(prims, o, d, np.float32(np.inf)), ranks)
+        got = _trace_wide(e, prims, ranks, o, d)
+        assert got[1] == brute[1] and got[0].view(np.uint32) == np.float32(brute[0]).view(np.uint32), (i, got, brute)
+        n_hit += got[1] >= 0
+    assert n_hit > 100
+
+
+def test_export_errors(host_scene):
+    with pytest.raises(RuntimeError):
+        host_scene.export("rebuilt", width=3)
+    with pytest.raises(RuntimeError):
+        host_scene.export("rebuilt", leaf_size=40)
+    with pytest.raises(ValueError):
+        host_scene.export("bogus")
