@@ -180,9 +180,10 @@ typedef struct crt_scene_options {
 /* ---- scene (SceneManager device half) ---- */
 /* Host-only: build the device arrays crt_scene_create_ex would upload and copy them out (no GPU needed;
  * used by the CPU tests to validate the rebuilt BVH).  Call with null arrays to get the sizes:
- * info = {node float4s, prim float4s, ranks, nodes per layout, layouts, width, stack bound, excluded}. */
+ * info = {node float4s, prim float4s, ranks, nodes per layout, layouts, width, stack bound, excluded,
+ *         first per-ray sphere prim, per-ray spheres}. */
 int  crt_scene_export(const crt_scene_desc* desc, const crt_scene_options* opts, float* nodes, float* prims,
-                      int32_t* rank_code, int64_t info[8]);
+                      int32_t* rank_code, int64_t info[10]);
 int  crt_scene_create(const crt_scene_desc* desc, int device, crt_scene** out);
 /* crt_scene_create with options (NULL = defaults = CRT_BVH_REFERENCE). */
 int  crt_scene_create_ex(const crt_scene_desc* desc, int device, const crt_scene_options* opts, crt_scene** out);
@@ -209,9 +210,16 @@ int  crt_renderer_set_camera(crt_renderer* r, const crt_camera_desc* cam);
  * with wave-cooperative leaf intersection; 2 = 1 + traversal-step scheduling with parked-lane
  * regeneration (lanes start their next ray without waiting for the wave's slowest trace); 3 = 2 +
  * next-node prefetch overlapping the leaf rounds.  Scenes with 4-wide nodes (CRT_BVH_REBUILT, width 4)
- * always use variant 4: the variant-3 scheduling over 4-wide nodes with a per-lane stack. */
+ * use variant 4 (the variant-3 scheduling over 4-wide nodes with a per-lane stack) unless variant 5 is
+ * selected: the wavefront path (trace and shade kernels over a queue of active pixels, same results). */
 int  crt_renderer_set_kernel_variant(crt_renderer* r, int variant);
-/* Variants 2-4: number of parked lanes (1..64, default 24) that triggers a shading/regeneration pass. */
+/* Variant 5: idle lanes that trigger a queue fetch in the trace kernel (1..64, default 16) and trace/shade
+ * iterations between host reads of the queue length (default 16).  Variant-5 renders return after the
+ * frame's kernels have been enqueued AND the queue has drained (host-synchronous). */
+int  crt_renderer_set_wavefront(crt_renderer* r, int refill_lanes, int check_iterations);
+long long crt_renderer_wavefront_iterations(const crt_renderer* r);   /* iterations of the last variant-5 render */
+/* Variants 2-4: number of parked lanes (1..64) that triggers a shading/regeneration pass; default 24 for
+ * variants 2/3 and 40 for variant 4 (setting it sets both). */
 int  crt_renderer_set_regen_threshold(crt_renderer* r, int lanes);
 /* Variant 4: per-lane traversal-stack entries kept in LDS (1..16, default 16); deeper entries spill to a
  * per-pixel region in HBM.  Results do not depend on it (tests force the HBM path with 1). */
@@ -235,6 +243,9 @@ int  crt_renderer_get_counters(crt_renderer* r, crt_work_counters* out);/* of th
  * crt_renderer_get_counters: [0] lane-slots of traversal steps (compare box_tests), [1] lane-slots
  * of cooperative leaf rounds (compare tri_tests), [2] wave-level trace calls. */
 int  crt_renderer_get_schedule_stats(crt_renderer* r, unsigned long long* out3);
+/* Section profile of the last counting render (variant 4), summed over waves, shader-clock cycles:
+ * {shading/regeneration passes, traversal steps (box tests + stack), leaf rounds, passes, waves}. */
+int  crt_renderer_get_section_profile(crt_renderer* r, unsigned long long* out5);
 float* crt_renderer_linear_device_ptr(crt_renderer* r);   /* for RCCL reduce of the framebuffer */
 /* Bind the linear-sum framebuffer to caller-owned device memory of W*H*3 floats on the renderer's
  * device (e.g. a tensor the caller all-reduces with RCCL); NULL re-binds the internal buffer. */

@@ -118,7 +118,7 @@ class HostScene:
         """The device arrays crt_scene_create_ex would upload (host only, crt_scene_export)."""
         o = scene_options(bvh, **options)
         d = self.desc()
-        info = (C.c_int64 * 8)()
+        info = (C.c_int64 * 10)()
         check(_lib.hip().crt_scene_export(C.byref(d), C.byref(o), None, None, None, info), "crt_scene_export")
         nodes = np.zeros((info[0], 4), np.float32)
         prims = np.zeros((info[1], 4), np.float32)
@@ -126,7 +126,7 @@ class HostScene:
         check(_lib.hip().crt_scene_export(C.byref(d), C.byref(o), _p(nodes), _p(prims), _p(rank_code), info),
               "crt_scene_export")
         keys = ("node_float4s", "prim_float4s", "ranks", "nodes_per_layout", "layouts", "width", "stack_bound",
-                "excluded")
+                "excluded", "sphere_first", "n_ray_spheres")
         out = dict(zip(keys, (int(v) for v in info)))
         out.update(nodes=nodes, prims=prims, rank_code=rank_code)
         return out
@@ -204,6 +204,12 @@ class Renderer:
     def set_regen_threshold(self, lanes: int):
         check(_lib.hip().crt_renderer_set_regen_threshold(self.h, int(lanes)), "set_regen_threshold")
 
+    def set_wavefront(self, refill_lanes: int = 16, check_iterations: int = 16):
+        check(_lib.hip().crt_renderer_set_wavefront(self.h, int(refill_lanes), int(check_iterations)), "set_wavefront")
+
+    def wavefront_iterations(self) -> int:
+        return int(_lib.hip().crt_renderer_wavefront_iterations(self.h))
+
     def set_stack_lds(self, entries: int):
         check(_lib.hip().crt_renderer_set_stack_lds(self.h, int(entries)), "set_stack_lds")
 
@@ -250,6 +256,12 @@ class Renderer:
         a = (C.c_ulonglong * 3)()
         check(_lib.hip().crt_renderer_get_schedule_stats(self.h, a), "get_schedule_stats")
         return {"step_lane_slots": int(a[0]), "round_lane_slots": int(a[1]), "wave_trace_calls": int(a[2])}
+
+    def section_profile(self) -> dict:
+        """Shader-clock cycles per section of the last counting render (variant 4), summed over waves."""
+        a = (C.c_ulonglong * 5)()
+        check(_lib.hip().crt_renderer_get_section_profile(self.h, a), "get_section_profile")
+        return dict(zip(("cyc_regen", "cyc_step", "cyc_round", "passes", "waves"), (int(v) for v in a)))
 
     def last_kernel_ms(self) -> float:
         return float(_lib.hip().crt_renderer_last_kernel_ms(self.h))

@@ -48,6 +48,7 @@ struct RenderParams {
     uint32_t* __restrict__ ovf;           // variant 4: traversal-stack entries beyond the LDS part
     int stack_cap;                        // variant 4: stack entries a ray can need (host bound)
     int stack_lds;                        // variant 4: entries kept in LDS (<= STACK_LDS; rest in ovf)
+    int sphere_first, n_ray_spheres;      // variant 4: spheres tested per ray at generation (not in the BVH)
     unsigned* err;                // device error flag (bit 0: primitive index out of range)
     int width, height, spp, max_bounces;
     int accumulate;
@@ -58,7 +59,12 @@ struct RenderParams {
     crt_camera_desc cam;
 };
 
-struct TraceCounts { uint32_t boxes, tris, spheres, step_slots, round_slots, trace_calls; };
+struct TraceCounts {
+    uint32_t boxes, tris, spheres, step_slots, round_slots, trace_calls;
+    // COUNT-mode section profile (variant 4; wave-uniform shader-clock cycles, s_memtime)
+    uint64_t cyc_regen, cyc_step, cyc_round, passes;
+};
+__device__ __forceinline__ uint64_t shader_clock() { return __builtin_amdgcn_s_memtime(); }
 
 // Hit rule shared by every variant and both BVH modes: a candidate (t, rank) replaces the current hit
 // when t < closest, or t == closest and its reference DFS rank is higher.  In CRT_BVH_REFERENCE mode the
@@ -526,6 +532,22 @@ __device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ q, V3 o, 
     return w;
 }
 
+// Spheres kept out of a 4-wide BVH (scenes with few spheres) are tested once per ray, before the traversal;
+// the hit rule is order-independent, so this is the same closest hit.
+__device__ __forceinline__ void ray_spheres(const float4* __restrict__ prims, int first, int n, V3 o, V3 d,
+                                            float& closest, int& hit) {
+    for (int s = 0; s < n; ++s) {
+        const int p = first + s;
+        const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1];
+        const float t = sphere_candidate(f0, f1, o, d, __builtin_inff());
+        const int rank = __float_as_int(f1.z);
+        if (t >= 0.f && better(t, rank, closest, hit)) {
+            closest = t;
+            hit = rank;
+        }
+    }
+}
+
 __device__ __forceinline__ void cas(uint32_t& a, uint32_t& b) {
     const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
     a = lo;
@@ -533,11 +555,12 @@ __device__ __forceinline__ void cas(uint32_t& a, uint32_t& b) {
 }
 
 // Per-lane closest hit over a 4-wide BVH (diagnostic path: crt_scene_compare).  Returns the rank or -1.
-__device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict__ prims, V3 o, V3 d,
-                      float& closest) {
+__device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict__ prims, int sphere_first,
+                      int n_spheres, V3 o, V3 d, float& closest) {
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     closest = __builtin_inff();
     int hit = -1, node = 0, sp = 0;
+    ray_spheres(prims, sphere_first, n_spheres, o, d, closest, hit);
     int stack[64];
     while (node >= 0) {
         const float4* q = nodes + 8 * (size_t)node;
@@ -581,6 +604,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
                                                float& closest, int& hit, TraceCounts& cnt, WaveLds& L,
                                                uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix) {
     if (COUNT) cnt.step_slots++;
+    const uint64_t c0 = COUNT ? shader_clock() : 0;
     int leaf_n = 0, leaf_first = 0;
     if (node >= 0) {
         const float4* q = P.nodes + 8 * (size_t)node;
@@ -629,6 +653,8 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
             node = -1;
         }
     }
+    const uint64_t c1 = COUNT ? shader_clock() : 0;
+    if (COUNT) cnt.cyc_step += c1 - c0;
     if (!__ballot(leaf_n > 0)) return;
     const int incl = wave_inclusive_scan(leaf_n, lane);
     const int total = __builtin_amdgcn_readlane(incl, 63);
@@ -673,6 +699,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
             hit = rank;
         }
     }
+    if (COUNT) cnt.cyc_round += shader_clock() - c1;
 }
 
 // Per-lane path state of one pixel (rayColor's locals, CUDAKernels.h:102-145, plus the sample loop).
@@ -814,7 +841,9 @@ __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int h
 template <bool COUNT, int VARIANT, int MINW>
 __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
     __shared__ WaveLds lds[VARIANT >= 1 ? 4 : 1];
-    __shared__ uint32_t stack_lds[VARIANT == 4 ? 4 * STACK_LDS * 64 : 1];
+    // variant 4: 16 LDS stack entries per lane at 5 waves/SIMD; 12 at 6+ so 6 workgroups fit the 160 KiB
+    constexpr int SD = VARIANT == 4 ? (MINW >= 6 ? 12 : STACK_LDS) : 1;
+    __shared__ uint32_t stack_lds[VARIANT == 4 ? 4 * SD * 64 : 1];
     // 16x16 pixel tile per workgroup, 8x8 per wave64.
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -845,7 +874,7 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
     C.lens = Cd.lens_radius;
     C.fw = (float)P.width;
     C.fh = (float)P.height;
-    TraceCounts cnt{0, 0, 0, 0, 0, 0};
+    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
     if (VARIANT == 0) {
         for (;;) {
@@ -859,7 +888,7 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
     } else if (VARIANT == 4) {
         // Same scheduling as variant 3 over a 4-wide BVH: node < 0 = no node left (lane parked).
         WaveLds& L = lds[wave];
-        uint32_t* stk = stack_lds + wave * STACK_LDS * 64;
+        uint32_t* stk = stack_lds + wave * SD * 64;
         const float INF = __builtin_inff();
         const size_t n_pix = (size_t)P.width * P.height;
         bool live = true, has_result = false;
@@ -872,7 +901,9 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
             const int n_parked = __popcll(__ballot(parked));
             const int n_live = __popcll(__ballot(live));
             if (n_live == 0) break;
+            const uint64_t c0 = COUNT ? shader_clock() : 0;
             if (n_parked >= P.regen_threshold || n_parked == n_live) {
+                if (COUNT) cnt.passes++;
                 if (parked) {
                     if (has_result) shade(S, P, hit, closest);
                     live = next_ray(S, C, x, y, P.max_bounces);
@@ -886,11 +917,14 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
                         hit = -1;
                         // conservative traversal only needs 1/d to within an ulp (boxes are padded)
                         inv = v3(__builtin_amdgcn_rcpf(S.d.x), __builtin_amdgcn_rcpf(S.d.y), __builtin_amdgcn_rcpf(S.d.z));
+                        ray_spheres(P.prims, P.sphere_first, P.n_ray_spheres, S.o, S.d, closest, hit);
+                        if (COUNT) cnt.spheres += P.n_ray_spheres;
                         L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                         if (COUNT) cnt.trace_calls++;
                     }
                 }
             }
+            if (COUNT) cnt.cyc_regen += shader_clock() - c0;
             traverse_step4<COUNT>(P, S.o, S.d, inv, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
         }
     } else if (VARIANT == 2 || VARIANT == 3) {
@@ -971,9 +1005,246 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
             // and wave-level trace calls (all uniform per wave)
             atomicAdd(&P.counters[5], 64ull * cnt.step_slots);
             atomicAdd(&P.counters[6], 64ull * cnt.round_slots + ((unsigned long long)cnt.trace_calls << 40));
+            atomicAdd(&P.counters[8], (unsigned long long)cnt.cyc_regen);
+            atomicAdd(&P.counters[9], (unsigned long long)cnt.cyc_step);
+            atomicAdd(&P.counters[10], (unsigned long long)cnt.cyc_round);
+            atomicAdd(&P.counters[11], (unsigned long long)cnt.passes);
+            atomicAdd(&P.counters[12], 1ull);
         }
     }
     if (lane == 0) atomicAdd(&P.counters[0], (unsigned long long)wr);
+}
+
+// ------------------------------------------------------------------ wavefront path (variant 5)
+// Trace and shade as separate kernels over a queue of active pixels (4-wide BVH scenes).  Each pixel has
+// at most one path in flight and its samples stay in order, so every pixel's RNG stream and sum evolve
+// exactly as in the megakernels.  Per-pixel state lives in HBM between the phases:
+//   ray[2p], ray[2p+1] = (o.xyz, d.x), (d.y, d.z, t, hit rank)   path[p] = (thr.xyz, bounce)
+//   remaining[p] = samples not started; rng / sum as for the megakernels.
+struct WfParams {
+    RenderParams P;
+    float4* __restrict__ ray;
+    float4* __restrict__ path;
+    int* __restrict__ remaining;
+    const int* __restrict__ queue_in;
+    int* __restrict__ queue_out;
+    const int* __restrict__ count_in;
+    int* __restrict__ count_out;
+    int* __restrict__ head;      // trace: queue fetch cursor
+    int initial;                 // shade: first pass of the launch (no hit to shade)
+    int refill;                  // trace: idle lanes that trigger a queue fetch
+};
+
+constexpr int WF_STACK = 16;     // trace kernel: per-lane stack entries in LDS (deeper ones in P.ovf)
+
+__device__ __forceinline__ CamRegs cam_regs(const RenderParams& P) {
+    const crt_camera_desc& Cd = P.cam;
+    CamRegs C;
+    C.pos = v3(Cd.origin[0], Cd.origin[1], Cd.origin[2]);
+    C.llc = v3(Cd.lower_left[0], Cd.lower_left[1], Cd.lower_left[2]);
+    C.hor = v3(Cd.horizontal[0], Cd.horizontal[1], Cd.horizontal[2]);
+    C.ver = v3(Cd.vertical[0], Cd.vertical[1], Cd.vertical[2]);
+    C.right = v3(Cd.right[0], Cd.right[1], Cd.right[2]);
+    C.up = v3(Cd.up[0], Cd.up[1], Cd.up[2]);
+    C.lens = Cd.lens_radius;
+    C.fw = (float)P.width;
+    C.fh = (float)P.height;
+    return C;
+}
+
+// Streaming per-pixel state: non-temporal so it does not push the scene out of L2.
+template <typename T> __device__ __forceinline__ T ld_nt(const T* p) { return __builtin_nontemporal_load(p); }
+template <typename T> __device__ __forceinline__ void st_nt(T v, T* p) { __builtin_nontemporal_store(v, p); }
+typedef float nf4 __attribute__((ext_vector_type(4)));
+typedef float nf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 ld_nt(const float4* p) {
+    const nf4 v = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt(float4 v, float4* p) {
+    const nf4 n = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(n, reinterpret_cast<nf4*>(p));
+}
+__device__ __forceinline__ void st_nt(float2 v, float2* p) {
+    const nf2 n = {v.x, v.y};
+    __builtin_nontemporal_store(n, reinterpret_cast<nf2*>(p));
+}
+
+constexpr int WF_CHUNK = 256;    // queue entries a trace wave claims per global atomic
+
+// Trace phase: persistent waves over the queue.  Each wave claims chunks of WF_CHUNK queue entries with one
+// atomic and feeds its lanes from the chunk; every lane keeps a two-stage prefetch (queue entry, then the
+// ray) so a lane whose trace ends swaps in an already-loaded ray at the next step.  The variant-4 step runs
+// on every wave iteration, so traversal steps stay full until the queue drains.
+template <bool COUNT>
+__global__ __launch_bounds__(256) void crt_wf_trace_kernel(WfParams W) {
+    const RenderParams& P = W.P;
+    __shared__ WaveLds lds[4];
+    __shared__ uint32_t stack_lds[4 * WF_STACK * 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    WaveLds& L = lds[wave];
+    uint32_t* stk = stack_lds + wave * WF_STACK * 64;
+    const int count = *W.count_in;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *W.count_out = 0;                                  // the shade phase appends to it next
+        atomicAdd(&P.counters[0], (unsigned long long)count);   // every queued pixel traces one ray
+    }
+    const size_t n_pix = (size_t)P.width * P.height;
+    const float INF = __builtin_inff();
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    int p = -1, node = -1, sp = 0, hit = -1;
+    float closest = INF;
+    V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
+    int nq = -1, np = -1;                                  // prefetch: queue entry loaded / ray loaded
+    float4 r0n = make_float4(0.f, 0.f, 0.f, 0.f), r1n = r0n;
+    int chunk_next = 0, chunk_end = 0;                     // wave-uniform
+    bool more = true;                                      // wave-uniform: the global queue may have entries
+    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    L.owner_at[lane] = 0xff;
+    for (;;) {
+        if (p < 0 && np >= 0) {                            // swap in the prefetched ray
+            p = np;
+            np = -1;
+            o = v3(r0n.x, r0n.y, r0n.z);
+            d = v3(r0n.w, r1n.x, r1n.y);
+            inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+            node = 0;
+            sp = 0;
+            closest = INF;
+            hit = -1;
+            ray_spheres(P.prims, P.sphere_first, P.n_ray_spheres, o, d, closest, hit);
+            if (COUNT) cnt.spheres += P.n_ray_spheres;
+            L.ray0[lane] = make_float4(o.x, o.y, o.z, d.x);
+        }
+        if (np < 0 && nq >= 0) {                           // stage 2: start the ray loads
+            np = nq;
+            nq = -1;
+            r0n = ld_nt(&W.ray[2 * (size_t)np]);
+            r1n = ld_nt(&W.ray[2 * (size_t)np + 1]);
+        }
+        const uint64_t need = __ballot(nq < 0 && np < 0);  // stage 1: lanes with an empty pipeline
+        const int n_need = __popcll(need);
+        if (n_need >= W.refill || n_need == 64) {
+            if (chunk_next >= chunk_end && more) {
+                int b = count;
+                if (lane == 0 && __hip_atomic_load(W.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < count)
+                    b = atomicAdd(W.head, WF_CHUNK);   // (skip the contended atomic once the queue is claimed)
+                b = __shfl(b, 0);
+                chunk_next = b;
+                chunk_end = min(b + WF_CHUNK, count);
+                if (b + WF_CHUNK >= count) more = false;
+            }
+            const int take = min(max(chunk_end - chunk_next, 0), n_need);
+            const int rank = __popcll(need & lt_mask);
+            if (((need >> lane) & 1ull) && rank < take) nq = ld_nt(&W.queue_in[chunk_next + rank]);
+            chunk_next += take;
+        }
+        if (!__ballot(p >= 0 || np >= 0 || nq >= 0)) {
+            if (!more && chunk_next >= chunk_end) break;
+            continue;
+        }
+        traverse_step4<COUNT>(P, o, d, inv, node, sp, closest, hit, cnt, L, stk, lane, p < 0 ? 0 : (size_t)p, n_pix);
+        if (p >= 0 && node < 0) {
+            st_nt(make_float2(closest, __int_as_float(hit)), reinterpret_cast<float2*>(&W.ray[2 * (size_t)p + 1].z));
+            p = -1;
+        }
+    }
+    if (COUNT) {
+        const uint64_t wb = wave_sum_u64(cnt.boxes), wt = wave_sum_u64(cnt.tris), ws = wave_sum_u64(cnt.spheres);
+        if (lane == 0) {
+            atomicAdd(&P.counters[1], (unsigned long long)wb);
+            atomicAdd(&P.counters[2], (unsigned long long)wt);
+            atomicAdd(&P.counters[3], (unsigned long long)ws);
+            atomicAdd(&P.counters[5], 64ull * cnt.step_slots);
+            atomicAdd(&P.counters[6], 64ull * cnt.round_slots);
+            atomicAdd(&P.counters[9], (unsigned long long)cnt.cyc_step);
+            atomicAdd(&P.counters[10], (unsigned long long)cnt.cyc_round);
+        }
+    }
+}
+
+// Shade phase: one queued pixel per lane (block-stride loop, uniform trip count per workgroup): shade the
+// traced hit, start the pixel's next ray (next bounce, or next sample), append the pixel to the next queue
+// while it has a ray to trace (one atomic per workgroup and loop iteration).
+template <bool COUNT>
+__global__ __launch_bounds__(256) void crt_wf_shade_kernel(WfParams W) {
+    const RenderParams& P = W.P;
+    __shared__ int s_cnt[4];
+    __shared__ int s_base;
+    const int n_pix = P.width * P.height;
+    const int count = W.initial ? n_pix : *W.count_in;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *W.head = 0;         // fetch cursor of the next trace phase
+    const CamRegs C = cam_regs(P);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t paths = 0;
+    const uint64_t c0 = COUNT ? shader_clock() : 0;
+    for (int base = blockIdx.x * 256; base < count; base += gridDim.x * 256) {
+        const int i = base + (int)threadIdx.x;
+        bool live = false;
+        int p = -1;
+        if (i < count) {
+            p = W.initial ? i : ld_nt(&W.queue_in[i]);
+            const int x = p % P.width, y = p / P.width;
+            PathState S;
+            uint32_t* rw = P.rng + 6 * (size_t)p;
+            S.s = Rng{ld_nt(rw), ld_nt(rw + 1), ld_nt(rw + 2), ld_nt(rw + 3), ld_nt(rw + 4), ld_nt(rw + 5)};
+            S.rays = 0;
+            S.paths = 0;
+            float* sw = P.sum + 3 * (size_t)p;
+            if (W.initial) {
+                S.pixel = P.accumulate ? v3(ld_nt(sw), ld_nt(sw + 1), ld_nt(sw + 2)) : v3(0.f, 0.f, 0.f);
+                S.o = v3(0, 0, 0); S.d = v3(0, 0, 1); S.thr = v3(1, 1, 1);
+                S.bounce = 0;
+                S.remaining = P.spp;
+                S.need_new = true;
+                live = next_ray(S, C, x, y, P.max_bounces);
+            } else {
+                S.pixel = v3(ld_nt(sw), ld_nt(sw + 1), ld_nt(sw + 2));
+                const float4 r0 = ld_nt(&W.ray[2 * (size_t)p]), r1 = ld_nt(&W.ray[2 * (size_t)p + 1]);
+                const float4 pa = ld_nt(&W.path[p]);
+                S.o = v3(r0.x, r0.y, r0.z);
+                S.d = v3(r0.w, r1.x, r1.y);
+                S.thr = v3(pa.x, pa.y, pa.z);
+                S.bounce = __float_as_int(pa.w);
+                S.remaining = ld_nt(&W.remaining[p]);
+                S.need_new = false;
+                shade(S, P, __float_as_int(r1.w), r1.z);
+                live = next_ray(S, C, x, y, P.max_bounces);
+            }
+            st_nt(S.s.v0, rw); st_nt(S.s.v1, rw + 1); st_nt(S.s.v2, rw + 2);
+            st_nt(S.s.v3, rw + 3); st_nt(S.s.v4, rw + 4); st_nt(S.s.d, rw + 5);
+            st_nt(S.pixel.x, sw); st_nt(S.pixel.y, sw + 1); st_nt(S.pixel.z, sw + 2);
+            st_nt(S.remaining, &W.remaining[p]);
+            paths += S.paths;
+            if (live) {
+                st_nt(make_float4(S.o.x, S.o.y, S.o.z, S.d.x), &W.ray[2 * (size_t)p]);
+                st_nt(make_float4(S.d.y, S.d.z, 0.f, 0.f), &W.ray[2 * (size_t)p + 1]);
+                st_nt(make_float4(S.thr.x, S.thr.y, S.thr.z, __int_as_float(S.bounce)), &W.path[p]);
+            }
+        }
+        // append this workgroup's live pixels to the next queue with one atomic
+        const uint64_t m = __ballot(live);
+        if (lane == 0) s_cnt[wave] = __popcll(m);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+            s_base = tot ? atomicAdd(W.count_out, tot) : 0;
+        }
+        __syncthreads();
+        int off = s_base;
+        for (int w = 0; w < wave; ++w) off += s_cnt[w];
+        if (live) st_nt(p, &W.queue_out[off + __popcll(m & ((1ull << lane) - 1ull))]);
+        __syncthreads();
+    }
+    if (COUNT) {
+        const uint64_t wp = wave_sum_u64(paths);
+        if (lane == 0) {
+            atomicAdd(&P.counters[4], (unsigned long long)wp);
+            atomicAdd(&P.counters[8], (unsigned long long)(shader_clock() - c0));
+            atomicAdd(&P.counters[11], 1ull);
+        }
+    }
 }
 
 // Diagnostic: paths follow scene A (variant-0 trace); every ray is ALSO traced through scene B and the two
@@ -985,6 +1256,7 @@ struct CompareParams {
     const float4* __restrict__ prims_b;
     int n_nodes_b, n_layouts_b;
     int width_a, width_b;
+    int sphere_first_b, n_spheres_b;
 };
 
 __global__ __launch_bounds__(256) void crt_compare_kernel(CompareParams Q) {
@@ -1012,15 +1284,15 @@ __global__ __launch_bounds__(256) void crt_compare_kernel(CompareParams Q) {
     C.lens = Cd.lens_radius;
     C.fw = (float)P.width;
     C.fh = (float)P.height;
-    TraceCounts cnt{0, 0, 0, 0, 0, 0};
+    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long n_rank = 0, n_t = 0, n_bmiss = 0, n_amiss = 0;
     while (next_ray(S, C, x, y, P.max_bounces)) {
         ++S.rays;
         float ta, tb;
-        const int ha = Q.width_a == 4 ? trace4(P.nodes, P.prims, S.o, S.d, ta)
+        const int ha = Q.width_a == 4 ? trace4(P.nodes, P.prims, P.sphere_first, P.n_ray_spheres, S.o, S.d, ta)
                                       : trace<false>(P.nodes, P.prims, P.n_nodes, layout_base(S.d, P.n_layouts, P.n_nodes),
                                                      S.o, S.d, ta, cnt);
-        const int hb = Q.width_b == 4 ? trace4(Q.nodes_b, Q.prims_b, S.o, S.d, tb)
+        const int hb = Q.width_b == 4 ? trace4(Q.nodes_b, Q.prims_b, Q.sphere_first_b, Q.n_spheres_b, S.o, S.d, tb)
                                       : trace<false>(Q.nodes_b, Q.prims_b, Q.n_nodes_b,
                                                      layout_base(S.d, Q.n_layouts_b, Q.n_nodes_b), S.o, S.d, tb, cnt);
         if (ha != hb) {
@@ -1336,15 +1608,22 @@ struct Rebuilt {
 
     int width = 2;
     int stack_bound = 0;   // width 4: most stack entries any traversal can hold
+    int sphere_first = 0, n_ray_spheres = 0;   // width 4: spheres kept out of the tree (tested per ray)
+    static constexpr int kMaxRaySpheres = 8;
 
     bool build(const Flattener& F, int leaf_size, int layouts, float trav_cost, int wide) {
         width = wide;
         const int n = (int)(F.prims.size() / 3);
         std::vector<crt_sah::Item> items;
         items.reserve(n);
+        std::vector<int> ray_sph;
+        int n_sph = 0;
+        for (int p = 0; p < n; ++p) n_sph += (F.rank_code[F.rank_of[p]] & SPHERE_BIT) != 0;
+        const bool spheres_per_ray = width == 4 && n_sph <= kMaxRaySpheres;
         for (int p = 0; p < n; ++p) {
             const bool sphere = (F.rank_code[F.rank_of[p]] & SPHERE_BIT) != 0;
             if (!F.reachable[p]) { excluded += !sphere; continue; }
+            if (sphere && spheres_per_ray) { ray_sph.push_back(p); continue; }
             const float4 f0 = F.prims[3 * p], f1 = F.prims[3 * p + 1], f2 = F.prims[3 * p + 2];
             crt_sah::Item it;
             it.src = p;
@@ -1370,6 +1649,15 @@ struct Rebuilt {
             items.push_back(it);
         }
         rank_code.assign(F.rank_code.size(), 0);
+        auto append_ray_spheres = [&]() {
+            sphere_first = (int)(prims.size() / 3);
+            for (int p : ray_sph) {
+                const int np = (int)(prims.size() / 3);
+                for (int q = 0; q < 3; ++q) prims.push_back(F.prims[3 * p + q]);
+                rank_code[F.rank_of[p]] = SPHERE_BIT | np;
+            }
+            n_ray_spheres = (int)ray_sph.size();
+        };
         if (items.empty()) {   // nothing hittable: one empty-box node that no ray enters
             const float lo[3] = {0, 0, 0};
             prims.assign(3, make_float4(0, 0, 0, 0));
@@ -1378,13 +1666,26 @@ struct Rebuilt {
                 nodes.push_back(make_float4(lo[1], lo[2], i2f(1), i2f(NODE_MESH_INNER)));
             }
             n_nodes = 1;
+            if (width == 4) {   // a 4-wide root with no slots
+                nodes.clear();
+                for (int r = 0; r < 6; ++r) nodes.push_back(make_float4(1e30f, 1e30f, 1e30f, 1e30f));
+                nodes.push_back(make_float4(i2f(0), i2f(0), i2f(0), i2f(0)));
+                nodes.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+                prims.clear();
+                append_ray_spheres();
+                stack_bound = 1;
+            }
             return true;
         }
         crt_sah::Builder B(std::move(items), leaf_size, trav_cost);
         B.build();
         max_depth = B.max_depth();
         const auto& its = B.items();
-        if (width == 4) return emit4(F, B.nodes(), its);
+        if (width == 4) {
+            if (!emit4(F, B.nodes(), its)) return false;
+            append_ray_spheres();
+            return true;
+        }
         prims.resize(3 * its.size());
         for (size_t i = 0; i < its.size(); ++i) {
             const int p = its[i].src;
@@ -1494,6 +1795,7 @@ struct crt_scene {
     int bvh = CRT_BVH_REFERENCE, layouts = 1;
     int width = 2;                 // 2: threaded layouts (variants 0-3); 4: 4-wide nodes (variant 4)
     int stack_cap = 0;             // width 4: traversal-stack entries a ray can need
+    int sphere_first = 0, n_ray_spheres = 0;   // width 4: spheres tested per ray, prims [first, first + n)
     long excluded = 0;
 };
 
@@ -1511,11 +1813,24 @@ struct crt_renderer {
     bool timed = false;
     int variant = 3;               // see crt_renderer_set_kernel_variant
     unsigned long long diag[3] = {0, 0, 0};
-    int regen_threshold = 24;
+    unsigned long long prof[5] = {0, 0, 0, 0, 0};   // COUNT-mode section profile (variant 4)
+    int regen_threshold = 24;      // variants 2/3
+    int regen_threshold_wide = 40; // variant 4 (measured optimum on the 4-wide BVH, profiles/r01d)
     int min_waves = 5;             // variant 2 occupancy target: 1 (compiler's choice), 5, 6 or 8
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
     size_t ovf_entries = 0;
     int stack_lds = STACK_LDS;     // variant 4: per-lane stack entries kept in LDS
+    // variant 5 (wavefront) state, allocated on first use
+    float4* d_wf_ray = nullptr;
+    float4* d_wf_path = nullptr;
+    int* d_wf_rem = nullptr;
+    int* d_wf_queue = nullptr;     // 2 x W*H
+    int* d_wf_ctr = nullptr;       // count[0], count[1], head
+    int* h_wf_count = nullptr;     // pinned
+    int wf_refill = 16;
+    int wf_check = 16;             // iterations between host checks of the queue length
+    int n_cu = 0;
+    long long wf_iterations = 0;
 };
 
 namespace {
@@ -1579,7 +1894,7 @@ static int build_scene_arrays(const crt_scene_desc* D, const crt_scene_options* 
 extern "C" {
 
 int crt_scene_export(const crt_scene_desc* D, const crt_scene_options* opts, float* nodes, float* prims,
-                     int32_t* rank_code, int64_t info[8]) {
+                     int32_t* rank_code, int64_t info[10]) {
     if (!D || !info) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
     crt_scene_options o;
     Flattener F{D};
@@ -1597,6 +1912,8 @@ int crt_scene_export(const crt_scene_desc* D, const crt_scene_options* opts, flo
     info[5] = rebuilt ? RB.width : 2;
     info[6] = rebuilt ? RB.stack_bound : 0;
     info[7] = rebuilt ? RB.excluded : 0;
+    info[8] = rebuilt ? RB.sphere_first : 0;
+    info[9] = rebuilt ? RB.n_ray_spheres : 0;
     if (nodes) std::memcpy(nodes, N.data(), N.size() * sizeof(float4));
     if (prims) std::memcpy(prims, Pr.data(), Pr.size() * sizeof(float4));
     if (rank_code) std::memcpy(rank_code, rc.data(), rc.size() * sizeof(int));
@@ -1632,6 +1949,8 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
     S->excluded = rebuilt ? RB.excluded : 0;
     S->width = rebuilt ? RB.width : 2;
     S->stack_cap = rebuilt ? RB.stack_bound : 0;
+    S->sphere_first = rebuilt ? RB.sphere_first : 0;
+    S->n_ray_spheres = rebuilt ? RB.n_ray_spheres : 0;
     auto up = [&](float4** dst, const std::vector<float4>& src) -> hipError_t {
         size_t bytes = std::max<size_t>(src.size(), 1) * sizeof(float4);
         hipError_t e = hipMalloc((void**)dst, bytes);
@@ -1694,11 +2013,11 @@ int crt_renderer_create(int width, int height, int device, crt_renderer** out) {
         (e = hipMalloc((void**)&R->d_sum_own, n * 3 * 4)) != hipSuccess ||
         (e = hipMalloc((void**)&R->d_rgba, n * 4)) != hipSuccess ||
         (e = hipMalloc((void**)&R->d_seq, tab.size() * 4)) != hipSuccess ||
-        (e = hipMalloc((void**)&R->d_counters, 8 * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMalloc((void**)&R->d_counters, 16 * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMemcpy(R->d_seq, tab.data(), tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemset(R->d_sum_own, 0, n * 3 * 4)) != hipSuccess ||
         (e = hipMemset(R->d_rgba, 0, n * 4)) != hipSuccess ||
-        (e = hipMemset(R->d_counters, 0, 8 * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMemset(R->d_counters, 0, 16 * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipEventCreate(&R->ev0)) != hipSuccess || (e = hipEventCreate(&R->ev1)) != hipSuccess) {
         crt_renderer_destroy(R);
         return set_error(e == hipErrorOutOfMemory ? CRT_ERR_OUT_OF_MEMORY : CRT_ERR_HIP,
@@ -1730,6 +2049,12 @@ void crt_renderer_destroy(crt_renderer* R) {
     if (R->d_seq) (void)hipFree(R->d_seq);
     if (R->d_counters) (void)hipFree(R->d_counters);
     if (R->d_ovf) (void)hipFree(R->d_ovf);
+    if (R->d_wf_ray) (void)hipFree(R->d_wf_ray);
+    if (R->d_wf_path) (void)hipFree(R->d_wf_path);
+    if (R->d_wf_rem) (void)hipFree(R->d_wf_rem);
+    if (R->d_wf_queue) (void)hipFree(R->d_wf_queue);
+    if (R->d_wf_ctr) (void)hipFree(R->d_wf_ctr);
+    if (R->h_wf_count) (void)hipHostFree(R->h_wf_count);
     if (R->ev0) (void)hipEventDestroy(R->ev0);
     if (R->ev1) (void)hipEventDestroy(R->ev1);
     delete R;
@@ -1746,7 +2071,7 @@ int crt_renderer_init_rand(crt_renderer* R, unsigned long long seed, unsigned lo
 }
 
 int crt_renderer_set_kernel_variant(crt_renderer* R, int variant) {
-    if (!R || variant < 0 || variant > 3) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant");
+    if (!R || variant < 0 || variant > 5) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant");
     R->variant = variant;
     return CRT_OK;
 }
@@ -1766,6 +2091,7 @@ int crt_renderer_set_stack_lds(crt_renderer* R, int entries) {
 int crt_renderer_set_regen_threshold(crt_renderer* R, int lanes) {
     if (!R || lanes < 1 || lanes > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "threshold must be 1..64");
     R->regen_threshold = lanes;
+    R->regen_threshold_wide = lanes;
     return CRT_OK;
 }
 
@@ -1776,6 +2102,84 @@ int crt_renderer_set_camera(crt_renderer* R, const crt_camera_desc* cam) {
     return CRT_OK;
 }
 
+// Variant 5 driver: initial shade pass (first ray of every pixel), then trace / shade pairs until the queue
+// is empty.  The queue length is read back every wf_check iterations (the only host synchronisation).
+static int render_wavefront(crt_renderer* R, RenderParams& P, bool cnt, hipStream_t st) {
+    const size_t n = (size_t)R->width * R->height;
+    if (!R->d_wf_ray) {
+        hipError_t e;
+        if ((e = hipMalloc((void**)&R->d_wf_ray, n * 32)) != hipSuccess ||
+            (e = hipMalloc((void**)&R->d_wf_path, n * 16)) != hipSuccess ||
+            (e = hipMalloc((void**)&R->d_wf_rem, n * 4)) != hipSuccess ||
+            (e = hipMalloc((void**)&R->d_wf_queue, 2 * n * 4)) != hipSuccess ||
+            (e = hipMalloc((void**)&R->d_wf_ctr, 4 * sizeof(int))) != hipSuccess ||
+            (e = hipHostMalloc((void**)&R->h_wf_count, sizeof(int))) != hipSuccess)
+            return set_error(CRT_ERR_HIP, std::string("wavefront buffers: ") + hipGetErrorString(e));
+        int dev_cu = 0;
+        HIP_TRY(hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, R->device));
+        R->n_cu = dev_cu > 0 ? dev_cu : 256;
+    }
+    WfParams W;
+    W.P = P;
+    W.ray = R->d_wf_ray;
+    W.path = R->d_wf_path;
+    W.remaining = R->d_wf_rem;
+    W.head = R->d_wf_ctr + 2;
+    W.refill = R->wf_refill;
+    int* q[2] = {R->d_wf_queue, R->d_wf_queue + n};
+    int* c[2] = {R->d_wf_ctr, R->d_wf_ctr + 1};
+    const dim3 block(256);
+    const dim3 g_trace(R->n_cu * 5), g_shade((unsigned)std::min<size_t>((n + 255) / 256, (size_t)R->n_cu * 8));
+    HIP_TRY(hipMemsetAsync(R->d_wf_ctr, 0, 4 * sizeof(int), st));
+    HIP_TRY(hipEventRecord(R->ev0, st));
+    W.initial = 1;
+    W.queue_in = nullptr;
+    W.count_in = c[1];
+    W.queue_out = q[0];
+    W.count_out = c[0];
+    if (cnt) hipLaunchKernelGGL((crt_wf_shade_kernel<true>), g_shade, block, 0, st, W);
+    else hipLaunchKernelGGL((crt_wf_shade_kernel<false>), g_shade, block, 0, st, W);
+    HIP_TRY(hipGetLastError());
+    W.initial = 0;
+    // every pixel's ray count is bounded: spp samples x (max_bounces + 1) segments, + slack
+    const long long max_iter = (long long)P.spp * (P.max_bounces + 2) + 4;
+    long long it = 0;
+    for (; it < max_iter; ++it) {
+        const int a = (int)(it & 1), b = a ^ 1;
+        W.queue_in = q[a];
+        W.count_in = c[a];
+        W.queue_out = q[b];
+        W.count_out = c[b];
+        if (cnt) {
+            hipLaunchKernelGGL((crt_wf_trace_kernel<true>), g_trace, block, 0, st, W);
+            hipLaunchKernelGGL((crt_wf_shade_kernel<true>), g_shade, block, 0, st, W);
+        } else {
+            hipLaunchKernelGGL((crt_wf_trace_kernel<false>), g_trace, block, 0, st, W);
+            hipLaunchKernelGGL((crt_wf_shade_kernel<false>), g_shade, block, 0, st, W);
+        }
+        HIP_TRY(hipGetLastError());
+        if ((it + 1) % R->wf_check == 0) {
+            HIP_TRY(hipMemcpyAsync(R->h_wf_count, c[b], sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            if (*R->h_wf_count == 0) { ++it; break; }
+        }
+    }
+    R->wf_iterations = it;
+    HIP_TRY(hipEventRecord(R->ev1, st));
+    R->timed = true;
+    return CRT_OK;
+}
+
+int crt_renderer_set_wavefront(crt_renderer* R, int refill_lanes, int check_iterations) {
+    if (!R || refill_lanes < 1 || refill_lanes > 64 || check_iterations < 1 || check_iterations > 4096)
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "refill 1..64, check 1..4096");
+    R->wf_refill = refill_lanes;
+    R->wf_check = check_iterations;
+    return CRT_OK;
+}
+
+long long crt_renderer_wavefront_iterations(const crt_renderer* R) { return R ? R->wf_iterations : -1; }
+
 int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bounces, unsigned flags, void* stream) {
     if (!R || !S) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
     if (!R->has_camera) return set_error(CRT_ERR_INVALID_ARGUMENT, "camera not set");
@@ -1783,7 +2187,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     if (S->device != R->device) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene and renderer on different devices");
     HIP_TRY(hipSetDevice(R->device));
     hipStream_t st = (hipStream_t)stream;
-    HIP_TRY(hipMemsetAsync(R->d_counters, 0, 8 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(R->d_counters, 0, 16 * sizeof(unsigned long long), st));
     RenderParams P;
     P.nodes = S->d_nodes; P.prims = S->d_prims; P.mats = S->d_mats; P.rank_code = S->d_rank_code;
     P.n_nodes = S->n_nodes; P.n_mats = S->n_mats; P.n_prims = S->n_prims; P.n_layouts = S->layouts;
@@ -1793,9 +2197,11 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     P.ovf = nullptr;
     P.stack_cap = S->stack_cap;
-    P.stack_lds = R->stack_lds;
-    if (S->width == 4 && S->stack_cap > R->stack_lds) {
-        const size_t need = (size_t)(S->stack_cap - R->stack_lds);
+    P.sphere_first = S->sphere_first;
+    P.n_ray_spheres = S->n_ray_spheres;
+    P.stack_lds = std::min(R->stack_lds, R->min_waves >= 6 ? 12 : STACK_LDS);
+    if (S->width == 4 && S->stack_cap > P.stack_lds) {
+        const size_t need = (size_t)(S->stack_cap - P.stack_lds);
         if (need > R->ovf_entries) {         // grow the overflow stack region (rarely needed)
             HIP_TRY(hipStreamSynchronize(st));
             if (R->d_ovf) (void)hipFree(R->d_ovf);
@@ -1807,16 +2213,33 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         P.ovf = R->d_ovf;
     }
     dim3 grid((R->width + 15) / 16, (R->height + 15) / 16), block(256);
-    HIP_TRY(hipEventRecord(R->ev0, st));
     const bool cnt = (flags & CRT_RENDER_COUNT_WORK) != 0;
-    P.regen_threshold = R->regen_threshold;
+    P.regen_threshold = S->width == 4 ? R->regen_threshold_wide : R->regen_threshold;
+    if (S->width == 4 && R->variant == 5) {
+        P.stack_lds = std::min(R->stack_lds, WF_STACK);
+        if (S->stack_cap > P.stack_lds) {
+            const size_t need = (size_t)(S->stack_cap - P.stack_lds);
+            if (need > R->ovf_entries) {
+                HIP_TRY(hipStreamSynchronize(st));
+                if (R->d_ovf) (void)hipFree(R->d_ovf);
+                R->d_ovf = nullptr;
+                R->ovf_entries = 0;
+                HIP_TRY(hipMalloc((void**)&R->d_ovf, need * R->width * R->height * 4));
+                R->ovf_entries = need;
+            }
+            P.ovf = R->d_ovf;
+        }
+        return render_wavefront(R, P, cnt, st);
+    }
+    HIP_TRY(hipEventRecord(R->ev0, st));
 #define CRT_LAUNCH(V, W)                                                                     \
     do {                                                                                     \
         if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, V, W>), grid, block, 0, st, P);  \
         else hipLaunchKernelGGL((crt_render_kernel<false, V, W>), grid, block, 0, st, P);     \
     } while (0)
     if (S->width == 4) {
-        if (R->min_waves >= 5) CRT_LAUNCH(4, 5);
+        if (R->min_waves >= 6) CRT_LAUNCH(4, 6);
+        else if (R->min_waves >= 5) CRT_LAUNCH(4, 5);
         else if (R->min_waves >= 4) CRT_LAUNCH(4, 4);
         else CRT_LAUNCH(4, 1);
     }
@@ -1847,7 +2270,7 @@ int crt_scene_compare(crt_renderer* R, const crt_scene* A, const crt_scene* B, i
     if (A->n_ranks != B->n_ranks) return set_error(CRT_ERR_INVALID_ARGUMENT, "scenes hold different primitive sets");
     if (spp < 0 || max_bounces < 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "negative spp / bounces");
     HIP_TRY(hipSetDevice(R->device));
-    HIP_TRY(hipMemset(R->d_counters, 0, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(R->d_counters, 0, 16 * sizeof(unsigned long long)));
     CompareParams Q;
     RenderParams& P = Q.A;
     P.nodes = A->d_nodes; P.prims = A->d_prims; P.mats = A->d_mats; P.rank_code = A->d_rank_code;
@@ -1858,6 +2281,8 @@ int crt_scene_compare(crt_renderer* R, const crt_scene* A, const crt_scene* B, i
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     Q.nodes_b = B->d_nodes; Q.prims_b = B->d_prims; Q.n_nodes_b = B->n_nodes; Q.n_layouts_b = B->layouts;
     Q.width_a = A->width; Q.width_b = B->width;
+    P.sphere_first = A->sphere_first; P.n_ray_spheres = A->n_ray_spheres;
+    Q.sphere_first_b = B->sphere_first; Q.n_spheres_b = B->n_ray_spheres;
     dim3 grid((R->width + 15) / 16, (R->height + 15) / 16), block(256);
     hipLaunchKernelGGL(crt_compare_kernel, grid, block, 0, 0, Q);
     HIP_TRY(hipGetLastError());
@@ -1917,11 +2342,17 @@ int crt_renderer_write_linear(crt_renderer* R, const float* in) {
 }
 int crt_renderer_get_counters(crt_renderer* R, crt_work_counters* out) {
     if (!R || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
-    unsigned long long c[8];
+    unsigned long long c[16];
     if (int rc = read_dev(R, c, R->d_counters, sizeof c)) return rc;
     R->diag[0] = c[5]; R->diag[1] = c[6] & ((1ull << 40) - 1); R->diag[2] = c[6] >> 40;
+    for (int i = 0; i < 5; ++i) R->prof[i] = c[8 + i];
     out->rays = c[0]; out->box_tests = c[1]; out->tri_tests = c[2]; out->sphere_tests = c[3]; out->paths = c[4];
     if (c[7]) return set_error(CRT_ERR_HIP, "render kernel reported an internal indexing error");
+    return CRT_OK;
+}
+int crt_renderer_get_section_profile(crt_renderer* R, unsigned long long* out5) {
+    if (!R || !out5) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    for (int i = 0; i < 5; ++i) out5[i] = R->prof[i];
     return CRT_OK;
 }
 int crt_renderer_get_schedule_stats(crt_renderer* R, unsigned long long* out3) {

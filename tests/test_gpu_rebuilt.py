@@ -137,3 +137,32 @@ def test_golden_fixture_rebuilt(rebuilt):
     g = np.load(Path(__file__).resolve().parent / "golden" / "cornell_bunny_64x36_16spp.npz")
     r = _frame(rebuilt["cornell_bunny", "w4"], 64, 36, 16, 20, crt_amd.camera(16))
     _compare(r.linear(), g["sum"], 16, 0.99)
+
+
+@pytest.mark.parametrize("refill", [1, 16, 64])
+def test_wavefront_equals_megakernel(rebuilt, refill):
+    """Variant 5 (trace / shade kernels over a pixel queue) == variant 4, bit for bit, incl. accumulate."""
+    w, h, spp = 160, 90, 8
+    cam = crt_amd.camera(spp)
+    dev = rebuilt["cornell_bunny", "w4"]
+    a = _frame(dev, w, h, spp, 20, cam, variant=3)
+    b = crt_amd.Renderer(w, h)
+    b.set_kernel_variant(5)
+    b.set_wavefront(refill, 4)
+    b.set_camera(cam)
+    b.init_rand(41)
+    b.render(dev, 3, 20)
+    b.render(dev, 5, 20, accumulate=True)
+    b.synchronize()
+    assert b.wavefront_iterations() > 0
+    assert np.array_equal(a.linear().view(np.uint32), b.linear().view(np.uint32))
+    assert np.array_equal(a.rng_state(), b.rng_state())
+    c = crt_amd.Renderer(w, h)
+    c.set_kernel_variant(5)
+    c.set_stack_lds(1)
+    c.set_camera(cam)
+    c.init_rand(41)
+    c.render(dev, spp, 20, count_work=True)
+    c.synchronize()
+    assert np.array_equal(a.linear().view(np.uint32), c.linear().view(np.uint32))
+    assert c.counters()["rays"] == a.counters()["rays"]

@@ -112,7 +112,10 @@ def _check_wide(e, prims):
                     plo, phi = _prim_box(prims[p])
                     assert (plo > lo).all() and (phi < hi).all(), "leaf box must strictly enclose (padding)"
                 off += c
-    assert (seen == 1).all(), "every primitive in exactly one leaf"
+    rs = slice(e["sphere_first"], e["sphere_first"] + e["n_ray_spheres"])
+    assert _is_sphere(e["prims"])[rs].all(), "per-ray list holds spheres only"
+    seen[rs] += 1
+    assert (seen == 1).all(), "every primitive in exactly one leaf or the per-ray sphere list"
     assert len(parent_of) == n
     # child node boxes inside their parent's slot box
     for child, pr in parent_of.items():
@@ -225,6 +228,9 @@ def _trace_wide(e, prims, ranks, o, d):
     with np.errstate(all="ignore"):
         inv = (F32(1) / d).astype(np.float32)
     closest, hit = np.float32(np.inf), -1
+    rs = slice(e["sphere_first"], e["sphere_first"] + e["n_ray_spheres"])
+    if e["n_ray_spheres"]:
+        closest, hit = _best(_prim_t(prims[rs], o, d, np.float32(np.inf)), ranks[rs])
     stack, node, steps = [], 0, 0
     while node >= 0:
         steps += 1
@@ -252,6 +258,12 @@ def _trace_wide(e, prims, ranks, o, d):
         else:
             node = stack.pop() if stack else -1
     return closest, hit
+
+
+def test_wide_export_spheres_per_ray(host_scene):
+    e = host_scene.export("rebuilt", width=4)
+    assert e["n_ray_spheres"] == 2          # the ground sphere and the small sphere (SceneManager::createWorld)
+    assert e["sphere_first"] * 3 + 3 * e["n_ray_spheres"] == len(e["prims"])
 
 
 def test_wide_traversal_equals_brute_force(host_scene):

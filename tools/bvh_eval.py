@@ -30,6 +30,7 @@ ap.add_argument("--bounces", type=int, default=20)
 ap.add_argument("--configs", default="w4:l4:t1,w4:l8:t2,w2:l16:t6",
                 help="comma list of w<width>:l<leaf size>:t<SAH traversal cost>[:L<layouts>][:o<occupancy>]")
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--no-compare", action="store_true")
 a = ap.parse_args()
 
 hs = crt_amd.HostScene(assets.scene_files(a.scene))
@@ -53,7 +54,7 @@ def frame(scene):
 
 def work(scene):
     r.init_rand(41)
-    r.render(scene, min(a.spp, 4), a.bounces, count_work=True)
+    r.render(scene, a.spp, a.bounces, count_work=True)
     r.synchronize()
     c = r.counters()
     return {k: round(c[k] / c["rays"], 3) for k in ("box_tests", "tri_tests", "sphere_tests")}
@@ -67,11 +68,14 @@ for cfg in a.configs.split(","):
         width, leaf, trav = int(f.get("w", 4)), int(f.get("l", 4)), float(f.get("t", 1))
         layouts, occ = int(f.get("L", 6 if width == 2 else 1)), int(f.get("o", 5))
         r.set_occupancy_target(occ)
+        r.set_regen_threshold(int(f.get("T", 24)))
+        r.set_kernel_variant(int(f.get("V", 3)))
+        r.set_wavefront(int(f.get("R", 16)), int(f.get("K", 16)))
         t = time.time()
         sc = hs.upload(0, bvh="rebuilt", leaf_size=leaf, layouts=layouts, traversal_cost=trav, width=width)
         build_s = time.time() - t
         r.init_rand(41)
-        cmp = r.compare(ref, sc, a.cmp_spp, a.bounces)
+        cmp = {"rays": 0, "rank_mismatch": 0} if a.no_compare else r.compare(ref, sc, a.cmp_spp, a.bounces)
         ms, rays, img = frame(sc)
         d = (img - img_ref) * scale
         out = {"config": cfg, "scene": a.scene, "build_upload_s": round(build_s, 3),
@@ -82,6 +86,14 @@ for cfg in a.configs.split(","):
                "image": {"pixels_bit_equal": float(np.mean(np.all(img == img_ref, axis=-1))),
                          "rms_per_channel": [float(x) for x in np.sqrt(np.mean(d.reshape(-1, 3) ** 2, axis=0))]}}
         out["schedule"] = r.schedule_stats()
+        out["wf_iterations"] = r.wavefront_iterations()
+        prof = r.section_profile()
+        tot = max(1, prof["cyc_regen"] + prof["cyc_step"] + prof["cyc_round"])
+        out["section_profile"] = dict(prof, frac_regen=round(prof["cyc_regen"] / tot, 3),
+                                      frac_step=round(prof["cyc_step"] / tot, 3),
+                                      frac_round=round(prof["cyc_round"] / tot, 3))
         print(json.dumps(out), flush=True)
         sc.close()
         r.set_occupancy_target(5)
+        r.set_regen_threshold(24)
+        r.set_kernel_variant(3)
