@@ -197,6 +197,10 @@ void crt_scene_destroy(crt_scene* scene);
  * same crt_scene_desc.  Synchronous. */
 int  crt_scene_compare(crt_renderer* r, const crt_scene* a, const crt_scene* b, int spp, int max_bounces,
                        uint64_t out[5]);
+/* As crt_scene_compare, also copying up to max_dump differing rays to dump (10 floats each:
+ * o.xyz, d.xyz, rank in a, rank in b (int bits), t in a, t in b). */
+int  crt_scene_compare_dump(crt_renderer* r, const crt_scene* a, const crt_scene* b, int spp, int max_bounces,
+                            uint64_t out[5], float* dump, int max_dump);
 
 /* ---- renderer (CUDARenderer) ---- */
 int  crt_renderer_create(int width, int height, int device, crt_renderer** out);

@@ -291,6 +291,16 @@ class Renderer:
         keys = ("rays", "rank_mismatch", "t_mismatch", "b_miss", "a_miss")
         return dict(zip(keys, (int(v) for v in out)))
 
+    def compare_dump(self, scene_a: Scene, scene_b: Scene, spp: int, max_bounces: int = 20, max_dump: int = 256):
+        """compare() plus the differing rays: array [n, 10] = o.xyz, d.xyz, rank_a, rank_b (int bits), t_a, t_b."""
+        out = (C.c_uint64 * 5)()
+        buf = np.zeros((max_dump, 10), np.float32)
+        check(_lib.hip().crt_scene_compare_dump(self.h, scene_a.h, scene_b.h, int(spp), int(max_bounces), out,
+                                                _p(buf), int(max_dump)), "crt_scene_compare_dump")
+        keys = ("rays", "rank_mismatch", "t_mismatch", "b_miss", "a_miss")
+        res = dict(zip(keys, (int(v) for v in out)))
+        return res, buf[:min(max_dump, res["rank_mismatch"])]
+
 
 def pixel_sample_scale(spp: int) -> float:
     """m_PixelSampleScale = 1.f / m_SamplesPerPixel (Camera.cuh:23), rounded to f32."""

@@ -74,7 +74,7 @@ class WorkCounters(C.Structure):
 
 # exported symbol lists (checked by tests against include/*.h)
 HIP_SYMBOLS = [
-    "crt_abi_version", "crt_last_error", "crt_device_count", "crt_scene_create", "crt_scene_create_ex", "crt_scene_get_stats", "crt_scene_compare", "crt_scene_export",
+    "crt_abi_version", "crt_last_error", "crt_device_count", "crt_scene_create", "crt_scene_create_ex", "crt_scene_get_stats", "crt_scene_compare", "crt_scene_compare_dump", "crt_scene_export",
     "crt_renderer_set_stack_lds", "crt_renderer_get_section_profile", "crt_renderer_set_wavefront",
     "crt_renderer_wavefront_iterations",
     "crt_scene_destroy", "crt_renderer_create", "crt_renderer_destroy", "crt_renderer_init_rand",
@@ -123,6 +123,7 @@ def hip():
             "crt_device_count": ([P], i32),
             "crt_scene_create": ([P, i32, P], i32), "crt_scene_create_ex": ([P, i32, P, P], i32),
             "crt_scene_compare": ([P, P, P, i32, i32, P], i32),
+            "crt_scene_compare_dump": ([P, P, P, i32, i32, P, P, i32], i32),
             "crt_scene_export": ([P, P, P, P, P, P], i32), "crt_renderer_set_stack_lds": ([P, i32], i32),
             "crt_renderer_get_section_profile": ([P, P], i32),
             "crt_renderer_set_wavefront": ([P, i32, i32], i32),

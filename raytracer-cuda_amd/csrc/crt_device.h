@@ -73,6 +73,12 @@ __device__ __forceinline__ float rcp_newton(float x) {
 __device__ __forceinline__ float recip_exact(float x) {
     return fabsf(x) < RCP_FAST_MAX ? rcp_newton(x) : 1.0f / x;
 }
+// 1.f / x for ANY x (the fast path only inside the exhaustively verified range).
+constexpr float RCP_FAST_MIN = 1e-8f;
+__device__ __forceinline__ float recip_exact_any(float x) {
+    const float a = fabsf(x);
+    return (a >= RCP_FAST_MIN && a < RCP_FAST_MAX) ? rcp_newton(x) : 1.0f / x;
+}
 
 // ------------------------------------------------------------------ XORWOW
 // cuRAND XORWOW (CUDA 12.5 curand_kernel.h: curand, _curand_uniform) — see DESIGN.md.

@@ -49,6 +49,8 @@ struct RenderParams {
     int stack_cap;                        // variant 4: stack entries a ray can need (host bound)
     int stack_lds;                        // variant 4: entries kept in LDS (<= STACK_LDS; rest in ovf)
     int sphere_first, n_ray_spheres;      // variant 4: spheres tested per ray at generation (not in the BVH)
+    const float4* __restrict__ sphere_chain;   // their reference scene-level leaf boxes (see ray_spheres)
+    int n_chain;                                // boxes in sphere_chain
     unsigned* err;                // device error flag (bit 0: primitive index out of range)
     int width, height, spp, max_bounces;
     int accumulate;
@@ -533,12 +535,31 @@ __device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ q, V3 o, 
 }
 
 // Spheres kept out of a 4-wide BVH (scenes with few spheres) are tested once per ray, before the traversal;
-// the hit rule is order-independent, so this is the same closest hit.
-__device__ __forceinline__ void ray_spheres(const float4* __restrict__ prims, int first, int n, V3 o, V3 d,
-                                            float& closest, int& hit) {
+// the hit rule is order-independent, so this is the same closest hit.  A sphere is reached only if the
+// reference's scene-level boxes on its path pass AABB::hit against [0.001, inf) with the exact 1/d: the
+// reference never tests a sphere whose box the ray's interval misses, and f32 roots of large spheres can
+// land outside the sphere's own box (a ray leaving the radius-999 ground sphere at t just above 0.001).
+// Every ancestor box contains the sphere's leaf box and AABB::hit is monotone in the box (f32 subtraction
+// and multiplication are monotone), so the leaf box alone decides: record word 7 = its index in chain.
+__device__ __forceinline__ bool ref_scene_box(float4 A, float4 B, V3 o, V3 inv) {
+    const float t0x = (A.x - o.x) * inv.x, t0y = (A.y - o.y) * inv.y, t0z = (A.z - o.z) * inv.z;
+    const float t1x = (A.w - o.x) * inv.x, t1y = (B.x - o.y) * inv.y, t1z = (B.y - o.z) * inv.z;
+    float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+    float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    tmin = fmaxf(tmin, 0.001f);
+    tmax = fminf(tmax, __builtin_inff());
+    return !(tmax <= tmin);
+}
+__device__ __forceinline__ void ray_spheres(const float4* __restrict__ prims, const float4* __restrict__ chain,
+                                            int n_chain, int first, int n, V3 o, V3 d, float& closest, int& hit) {
+    if (n == 0) return;
+    // AABB::hit's 1/d, bit-exact (rcp + Newton inside its exhaustively verified range, division outside)
+    const V3 inv = v3(recip_exact_any(d.x), recip_exact_any(d.y), recip_exact_any(d.z));
     for (int s = 0; s < n; ++s) {
         const int p = first + s;
         const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1];
+        const int k = __float_as_int(f1.w);
+        if (!ref_scene_box(chain[2 * k], chain[2 * k + 1], o, inv)) continue;
         const float t = sphere_candidate(f0, f1, o, d, __builtin_inff());
         const int rank = __float_as_int(f1.z);
         if (t >= 0.f && better(t, rank, closest, hit)) {
@@ -555,12 +576,13 @@ __device__ __forceinline__ void cas(uint32_t& a, uint32_t& b) {
 }
 
 // Per-lane closest hit over a 4-wide BVH (diagnostic path: crt_scene_compare).  Returns the rank or -1.
-__device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict__ prims, int sphere_first,
-                      int n_spheres, V3 o, V3 d, float& closest) {
+__device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict__ prims,
+                      const float4* __restrict__ chain, int n_chain, int sphere_first, int n_spheres, V3 o, V3 d,
+                      float& closest) {
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     closest = __builtin_inff();
     int hit = -1, node = 0, sp = 0;
-    ray_spheres(prims, sphere_first, n_spheres, o, d, closest, hit);
+    ray_spheres(prims, chain, n_chain, sphere_first, n_spheres, o, d, closest, hit);
     int stack[64];
     while (node >= 0) {
         const float4* q = nodes + 8 * (size_t)node;
@@ -597,8 +619,11 @@ __device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict
 
 // One wave traversal step over a 4-wide BVH (variant 4).  Every lane with a node tests its four child
 // boxes; hit internal children are ordered near-first (u32 sort of (tmin bits | slot) keys), the nearest
-// becomes the lane's next node and the others are pushed onto its stack; the primitives of the hit leaf
-// children (one consecutive range) join this step's cooperative leaf rounds.  All 64 lanes call it.
+// becomes the lane's next node and the others go onto its stack as ONE entry (children are consecutive
+// nodes): first_child << 8 | remaining << 6 | slot0 << 4 | slot1 << 2 | slot2, slots in pop order.  A pop
+// takes slot0 and rewrites the entry while slots remain, so the stack holds at most one entry per
+// branching ancestor.  The primitives of the hit leaf children (one consecutive range) join this step's
+// cooperative leaf rounds.  All 64 lanes call it.
 template <bool COUNT>
 __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d, V3 inv, int& node, int& sp,
                                                float& closest, int& hit, TraceCounts& cnt, WaveLds& L,
@@ -634,21 +659,27 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
 #pragma unroll
         for (int s = 0; s < 4; ++s) k[s] = (s < n_int && w.hit[s]) ? ((__float_as_uint(w.tmin[s]) & ~3u) | s) : ~0u;
         cas(k[0], k[1]); cas(k[2], k[3]); cas(k[0], k[2]); cas(k[1], k[3]); cas(k[1], k[2]);
-        auto push = [&](uint32_t v) {
-            if (sp < P.stack_lds) stk[sp * 64 + lane] = v;
-            else if (sp < P.stack_cap) P.ovf[(size_t)(sp - P.stack_lds) * n_pix + pix] = v;
+        auto store = [&](int at, uint32_t v) {
+            if (at < P.stack_lds) stk[at * 64 + lane] = v;
+            else if (at < P.stack_cap) P.ovf[(size_t)(at - P.stack_lds) * n_pix + pix] = v;
             else atomicOr(P.err, 2u);        // host stack bound violated: report, drop the entry
-            ++sp;
         };
         if (k[0] != ~0u) {
             node = first_child + (int)(k[0] & 3);
-            if (k[3] != ~0u) push((uint32_t)first_child + (k[3] & 3));
-            if (k[2] != ~0u) push((uint32_t)first_child + (k[2] & 3));
-            if (k[1] != ~0u) push((uint32_t)first_child + (k[1] & 3));
+            const uint32_t n_rest = (k[1] != ~0u) + (k[2] != ~0u) + (k[3] != ~0u);
+            if (n_rest) {
+                store(sp, ((uint32_t)first_child << 8) | (n_rest << 6) | ((k[1] & 3) << 4) | ((k[2] & 3) << 2) |
+                              (k[3] & 3));
+                ++sp;
+            }
         } else if (sp > 0) {
-            --sp;
-            node = sp < P.stack_lds ? (int)stk[sp * 64 + lane]
-                                    : (sp < P.stack_cap ? (int)P.ovf[(size_t)(sp - P.stack_lds) * n_pix + pix] : -1);
+            const int at = sp - 1;
+            const uint32_t top = at < P.stack_lds ? stk[at * 64 + lane]
+                                                  : (at < P.stack_cap ? P.ovf[(size_t)(at - P.stack_lds) * n_pix + pix] : 0u);
+            const uint32_t rest = (top >> 6) & 3;
+            node = (int)(top >> 8) + (int)((top >> 4) & 3);
+            if (rest <= 1) sp = at;
+            else store(at, (top & ~0xffu) | ((rest - 1) << 6) | ((top & 0xfu) << 2));
         } else {
             node = -1;
         }
@@ -917,7 +948,7 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
                         hit = -1;
                         // conservative traversal only needs 1/d to within an ulp (boxes are padded)
                         inv = v3(__builtin_amdgcn_rcpf(S.d.x), __builtin_amdgcn_rcpf(S.d.y), __builtin_amdgcn_rcpf(S.d.z));
-                        ray_spheres(P.prims, P.sphere_first, P.n_ray_spheres, S.o, S.d, closest, hit);
+                        ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d, closest, hit);
                         if (COUNT) cnt.spheres += P.n_ray_spheres;
                         L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                         if (COUNT) cnt.trace_calls++;
@@ -1113,7 +1144,7 @@ __global__ __launch_bounds__(256) void crt_wf_trace_kernel(WfParams W) {
             sp = 0;
             closest = INF;
             hit = -1;
-            ray_spheres(P.prims, P.sphere_first, P.n_ray_spheres, o, d, closest, hit);
+            ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, o, d, closest, hit);
             if (COUNT) cnt.spheres += P.n_ray_spheres;
             L.ray0[lane] = make_float4(o.x, o.y, o.z, d.x);
         }
@@ -1257,6 +1288,10 @@ struct CompareParams {
     int n_nodes_b, n_layouts_b;
     int width_a, width_b;
     int sphere_first_b, n_spheres_b;
+    const float4* chain_b;
+    int n_chain_b;
+    float* dump;          // optional: up to max_dump differing rays, 10 floats each
+    int max_dump;
 };
 
 __global__ __launch_bounds__(256) void crt_compare_kernel(CompareParams Q) {
@@ -1289,16 +1324,26 @@ __global__ __launch_bounds__(256) void crt_compare_kernel(CompareParams Q) {
     while (next_ray(S, C, x, y, P.max_bounces)) {
         ++S.rays;
         float ta, tb;
-        const int ha = Q.width_a == 4 ? trace4(P.nodes, P.prims, P.sphere_first, P.n_ray_spheres, S.o, S.d, ta)
+        const int ha = Q.width_a == 4 ? trace4(P.nodes, P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o,
+                                               S.d, ta)
                                       : trace<false>(P.nodes, P.prims, P.n_nodes, layout_base(S.d, P.n_layouts, P.n_nodes),
                                                      S.o, S.d, ta, cnt);
-        const int hb = Q.width_b == 4 ? trace4(Q.nodes_b, Q.prims_b, Q.sphere_first_b, Q.n_spheres_b, S.o, S.d, tb)
+        const int hb = Q.width_b == 4 ? trace4(Q.nodes_b, Q.prims_b, Q.chain_b, Q.n_chain_b, Q.sphere_first_b, Q.n_spheres_b, S.o,
+                                               S.d, tb)
                                       : trace<false>(Q.nodes_b, Q.prims_b, Q.n_nodes_b,
                                                      layout_base(S.d, Q.n_layouts_b, Q.n_nodes_b), S.o, S.d, tb, cnt);
         if (ha != hb) {
             ++n_rank;
             n_bmiss += (hb < 0);
             n_amiss += (ha < 0);
+            if (Q.dump) {
+                const unsigned slot = atomicAdd(reinterpret_cast<unsigned*>(P.counters + 6), 1u);
+                if ((int)slot < Q.max_dump) {
+                    float* q = Q.dump + 10 * (size_t)slot;
+                    q[0] = S.o.x; q[1] = S.o.y; q[2] = S.o.z; q[3] = S.d.x; q[4] = S.d.y; q[5] = S.d.z;
+                    q[6] = __int_as_float(ha); q[7] = __int_as_float(hb); q[8] = ta; q[9] = tb;
+                }
+            }
         } else if (ha >= 0 && __float_as_uint(ta) != __float_as_uint(tb)) {
             ++n_t;
         }
@@ -1609,6 +1654,7 @@ struct Rebuilt {
     int width = 2;
     int stack_bound = 0;   // width 4: most stack entries any traversal can hold
     int sphere_first = 0, n_ray_spheres = 0;   // width 4: spheres kept out of the tree (tested per ray)
+    std::vector<float4> chain;                 // their reference scene-level leaf boxes (2 float4 per box)
     static constexpr int kMaxRaySpheres = 8;
 
     bool build(const Flattener& F, int leaf_size, int layouts, float trav_cost, int wide) {
@@ -1651,10 +1697,19 @@ struct Rebuilt {
         rank_code.assign(F.rank_code.size(), 0);
         auto append_ray_spheres = [&]() {
             sphere_first = (int)(prims.size() / 3);
+            const int n_ref = F.count();
             for (int p : ray_sph) {
                 const int np = (int)(prims.size() / 3);
                 for (int q = 0; q < 3; ++q) prims.push_back(F.prims[3 * p + q]);
                 rank_code[F.rank_of[p]] = SPHERE_BIT | np;
+                // the sphere's leaf in the flattened reference scene and every scene-level node enclosing it
+                int leaf = -1;
+                for (int i = 0; i < n_ref && leaf < 0; ++i)
+                    if (i2i(F.nodes[2 * (size_t)i + 1].w) == (SPHERE_BIT | p)) leaf = i;
+                const float4 B = F.nodes[2 * (size_t)leaf + 1];
+                prims[3 * (size_t)np + 1].w = i2f((int)(chain.size() / 2));
+                chain.push_back(F.nodes[2 * (size_t)leaf]);
+                chain.push_back(make_float4(B.x, B.y, 0.f, 0.f));
             }
             n_ray_spheres = (int)ray_sph.size();
         };
@@ -1742,13 +1797,14 @@ private:
             nodes.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
         }
         n_nodes = (int)queue.size();
-        // stack bound: visiting a node pushes (hit internal children - 1); children are visited later
+        // stack bound: visiting a node with 2+ hit internal children pushes ONE entry (its remaining children)
+        if (n_nodes >= (1 << 24)) { err = "too many nodes for 24-bit stack entries"; return false; }
         std::vector<int> bound(n_nodes, 0);
         for (int n = n_nodes - 1; n >= 0; --n) {
             const int fc = i2i(nodes[8 * (size_t)n + 6].x), m = wide[n].n_internal;
             int b = 0;
             for (int s = 0; s < m; ++s) b = std::max(b, bound[fc + s]);
-            bound[n] = m > 0 ? b + m - 1 : 0;
+            bound[n] = b + (m >= 2 ? 1 : 0);
         }
         stack_bound = bound[0] + 1;
         return true;
@@ -1789,6 +1845,8 @@ struct crt_scene {
     float4* d_nodes = nullptr;
     float4* d_prims = nullptr;
     float4* d_mats = nullptr;
+    float4* d_chain = nullptr;     // width 4: reference scene-level boxes on the per-ray spheres' paths
+    int n_chain = 0;
     int* d_rank_code = nullptr;
     int n_nodes = 0, n_prims = 0, n_mats = 0, n_ranks = 0;   // n_nodes per layout
     int max_depth = 0;
@@ -1950,6 +2008,7 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
     S->width = rebuilt ? RB.width : 2;
     S->stack_cap = rebuilt ? RB.stack_bound : 0;
     S->sphere_first = rebuilt ? RB.sphere_first : 0;
+    S->n_chain = rebuilt ? (int)(RB.chain.size() / 2) : 0;
     S->n_ray_spheres = rebuilt ? RB.n_ray_spheres : 0;
     auto up = [&](float4** dst, const std::vector<float4>& src) -> hipError_t {
         size_t bytes = std::max<size_t>(src.size(), 1) * sizeof(float4);
@@ -1963,6 +2022,7 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
     if ((e = up(&S->d_nodes, rebuilt ? RB.nodes : F.nodes)) != hipSuccess ||
         (e = up(&S->d_prims, rebuilt ? RB.prims : F.prims)) != hipSuccess ||
         (e = up(&S->d_mats, mats)) != hipSuccess ||
+        (e = up(&S->d_chain, rebuilt ? RB.chain : std::vector<float4>())) != hipSuccess ||
         (e = hipMalloc((void**)&S->d_rank_code, std::max<size_t>(rc.size(), 1) * sizeof(int))) != hipSuccess ||
         (!rc.empty() && (e = hipMemcpy(S->d_rank_code, rc.data(), rc.size() * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)) {
         crt_scene_destroy(S);
@@ -1995,6 +2055,7 @@ void crt_scene_destroy(crt_scene* S) {
     if (S->d_prims) (void)hipFree(S->d_prims);
     if (S->d_mats) (void)hipFree(S->d_mats);
     if (S->d_rank_code) (void)hipFree(S->d_rank_code);
+    if (S->d_chain) (void)hipFree(S->d_chain);
     delete S;
 }
 
@@ -2199,6 +2260,8 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.stack_cap = S->stack_cap;
     P.sphere_first = S->sphere_first;
     P.n_ray_spheres = S->n_ray_spheres;
+    P.sphere_chain = S->d_chain;
+    P.n_chain = S->n_chain;
     P.stack_lds = std::min(R->stack_lds, R->min_waves >= 6 ? 12 : STACK_LDS);
     if (S->width == 4 && S->stack_cap > P.stack_lds) {
         const size_t need = (size_t)(S->stack_cap - P.stack_lds);
@@ -2261,8 +2324,15 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     return CRT_OK;
 }
 
+int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene* B, int spp, int max_bounces,
+                           uint64_t out[5], float* dump, int max_dump);
 int crt_scene_compare(crt_renderer* R, const crt_scene* A, const crt_scene* B, int spp, int max_bounces,
                       uint64_t out[5]) {
+    return crt_scene_compare_dump(R, A, B, spp, max_bounces, out, nullptr, 0);
+}
+
+int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene* B, int spp, int max_bounces,
+                           uint64_t out[5], float* dump, int max_dump) {
     if (!R || !A || !B || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
     if (!R->has_camera) return set_error(CRT_ERR_INVALID_ARGUMENT, "camera not set");
     if (A->device != R->device || B->device != R->device)
@@ -2281,8 +2351,18 @@ int crt_scene_compare(crt_renderer* R, const crt_scene* A, const crt_scene* B, i
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     Q.nodes_b = B->d_nodes; Q.prims_b = B->d_prims; Q.n_nodes_b = B->n_nodes; Q.n_layouts_b = B->layouts;
     Q.width_a = A->width; Q.width_b = B->width;
-    P.sphere_first = A->sphere_first; P.n_ray_spheres = A->n_ray_spheres;
-    Q.sphere_first_b = B->sphere_first; Q.n_spheres_b = B->n_ray_spheres;
+    Q.dump = nullptr;
+    Q.max_dump = 0;
+    float* d_dump = nullptr;
+    if (dump && max_dump > 0) {
+        HIP_TRY(hipMalloc((void**)&d_dump, (size_t)max_dump * 10 * sizeof(float)));
+        Q.dump = d_dump;
+        Q.max_dump = max_dump;
+    }
+    P.sphere_first = A->sphere_first; P.n_ray_spheres = A->n_ray_spheres; P.sphere_chain = A->d_chain;
+    P.n_chain = A->n_chain;
+    Q.sphere_first_b = B->sphere_first; Q.n_spheres_b = B->n_ray_spheres; Q.chain_b = B->d_chain;
+    Q.n_chain_b = B->n_chain;
     dim3 grid((R->width + 15) / 16, (R->height + 15) / 16), block(256);
     hipLaunchKernelGGL(crt_compare_kernel, grid, block, 0, 0, Q);
     HIP_TRY(hipGetLastError());
@@ -2290,6 +2370,12 @@ int crt_scene_compare(crt_renderer* R, const crt_scene* A, const crt_scene* B, i
     unsigned long long h[8];
     HIP_TRY(hipMemcpy(h, R->d_counters, sizeof h, hipMemcpyDeviceToHost));
     for (int i = 0; i < 5; ++i) out[i] = h[i];
+    if (d_dump) {
+        const size_t n = std::min<size_t>((size_t)max_dump, (size_t)(h[6] & 0xffffffffu));
+        hipError_t e = n ? hipMemcpy(dump, d_dump, n * 10 * sizeof(float), hipMemcpyDeviceToHost) : hipSuccess;
+        (void)hipFree(d_dump);
+        HIP_TRY(e);
+    }
     return CRT_OK;
 }
 

@@ -61,10 +61,15 @@ def test_rebuilt_structure(host_scene, ref_export, opts):
     codes = e["rank_code"]
     for p, r in enumerate(ranks):
         assert codes[r] & ~(1 << 30) == p
-    # reference primitive with the same rank has the same record (apart from nothing)
+    # the reference primitive with the same rank has the same record; per-ray spheres (width 4) also carry
+    # the index of their reference scene-level leaf box in word 7
     ref_prims = ref_export["prims"].reshape(-1, 3, 4)
     ref_idx = ref_export["rank_code"][ranks] & ~(1 << 30)
-    assert np.array_equal(prims.view(np.uint32), ref_prims[ref_idx].view(np.uint32))
+    got = prims.view(np.uint32).copy()
+    rs = slice(e["sphere_first"], e["sphere_first"] + e["n_ray_spheres"])
+    assert np.array_equal(got[rs, 1, 3], np.arange(e["n_ray_spheres"], dtype=np.uint32)), "leaf-box index"
+    got[rs, 1, 3] = 0
+    assert np.array_equal(got, ref_prims[ref_idx].view(np.uint32))
     if e["width"] == 4:
         _check_wide(e, prims)
     else:
@@ -127,12 +132,12 @@ def _check_wide(e, prims):
         for s in range(meta >> 8):
             assert q[0, s] >= lo[0] and q[2, s] >= lo[1] and q[4, s] >= lo[2]
             assert q[1, s] <= hi[0] and q[3, s] <= hi[1] and q[5, s] <= hi[2]
-    # stack bound = max over root paths of sum(internal children - 1), recomputed independently
+    # stack bound = max over root paths of the branching nodes (one entry per node), recomputed independently
     bound = np.zeros(n, np.int64)
     for i in range(n - 1, -1, -1):
         fc, meta = _i(nodes[i, 6])[:2]
         m = meta & 0xFF
-        bound[i] = (m - 1 + max(bound[fc + s] for s in range(m))) if m else 0
+        bound[i] = (max(bound[fc + s] for s in range(m)) if m else 0) + (1 if m >= 2 else 0)
     assert e["stack_bound"] == bound[0] + 1
 
 
@@ -294,3 +299,28 @@ def test_export_errors(host_scene):
         host_scene.export("rebuilt", leaf_size=40)
     with pytest.raises(ValueError):
         host_scene.export("bogus")
+
+
+def test_ground_sphere_box_culls_spurious_root():
+    """The rays that once differed (tests/golden/ground_sphere_rays.json): they start a hair inside the
+    radius-999 ground sphere, whose f32 far root lands just above t = 0.001 but outside the sphere's own
+    box, so the reference's scene-level AABB::hit never lets Sphere::hit run.  Per-ray spheres therefore
+    replay that box chain (ray_spheres); here the mechanism is checked in f32 on the host."""
+    import json
+    from pathlib import Path
+    g = json.loads((Path(__file__).resolve().parent / "golden" / "ground_sphere_rays.json").read_text())
+    c, r = np.array([0, -1000, 0], F32), F32(999)
+    lo, hi = c - r, c + r
+    for ray in g["rays"]:
+        o, d = np.array(ray["o"], F32), np.array(ray["d"], F32)
+        rec = np.zeros((1, 3, 4), F32)
+        rec[0, 0] = [c[0], c[1], c[2], r]
+        rec[0, 1, 0] = r * r
+        t = _sphere_all(rec, o, d, np.float32(np.inf))[0]
+        assert 0.001 <= t < 0.002 and np.float32(t) == np.float32(ray["rebuilt_t_before_fix"])
+        with np.errstate(all="ignore"):
+            inv = (F32(1) / d).astype(F32)
+            t0, t1 = ((lo - o) * inv).astype(F32), ((hi - o) * inv).astype(F32)
+        tmin = max(max(min(t0[0], t1[0]), min(t0[1], t1[1])), min(t0[2], t1[2]), F32(0.001))
+        tmax = min(max(t0[0], t1[0]), max(t0[1], t1[1]), max(t0[2], t1[2]))
+        assert tmax <= tmin, "the reference's sphere box test rejects the ray"
