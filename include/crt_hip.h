@@ -248,8 +248,9 @@ int  crt_renderer_get_counters(crt_renderer* r, crt_work_counters* out);/* of th
  * of cooperative leaf rounds (compare tri_tests), [2] wave-level trace calls. */
 int  crt_renderer_get_schedule_stats(crt_renderer* r, unsigned long long* out3);
 /* Section profile of the last counting render (variant 4), summed over waves, shader-clock cycles:
- * {shading/regeneration passes, traversal steps (box tests + stack), leaf rounds, passes, waves}. */
-int  crt_renderer_get_section_profile(crt_renderer* r, unsigned long long* out5);
+ * {shading/regeneration passes, traversal steps (box tests + stack), leaf rounds, passes, waves,
+ *  shade() inside the passes, next_ray() inside the passes}. */
+int  crt_renderer_get_section_profile(crt_renderer* r, unsigned long long* out7);
 float* crt_renderer_linear_device_ptr(crt_renderer* r);   /* for RCCL reduce of the framebuffer */
 /* Bind the linear-sum framebuffer to caller-owned device memory of W*H*3 floats on the renderer's
  * device (e.g. a tensor the caller all-reduces with RCCL); NULL re-binds the internal buffer. */

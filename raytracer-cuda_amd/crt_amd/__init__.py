@@ -259,9 +259,10 @@ class Renderer:
 
     def section_profile(self) -> dict:
         """Shader-clock cycles per section of the last counting render (variant 4), summed over waves."""
-        a = (C.c_ulonglong * 5)()
+        a = (C.c_ulonglong * 7)()
         check(_lib.hip().crt_renderer_get_section_profile(self.h, a), "get_section_profile")
-        return dict(zip(("cyc_regen", "cyc_step", "cyc_round", "passes", "waves"), (int(v) for v in a)))
+        return dict(zip(("cyc_regen", "cyc_step", "cyc_round", "passes", "waves", "cyc_shade", "cyc_next"),
+                        (int(v) for v in a)))
 
     def last_kernel_ms(self) -> float:
         return float(_lib.hip().crt_renderer_last_kernel_ms(self.h))

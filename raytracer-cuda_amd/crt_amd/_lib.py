@@ -14,7 +14,8 @@ from pathlib import Path
 PKG_ROOT = Path(__file__).resolve().parents[1]          # raytracer-cuda_amd/
 REPO = PKG_ROOT.parent
 LIB_DIR = PKG_ROOT / "lib"
-HIP_LIB = LIB_DIR / "libcrt_hip.so"
+# CRT_HIP_LIB: an alternative build of the same library (A/B profiling builds, tools/); default in-tree
+HIP_LIB = Path(os.environ["CRT_HIP_LIB"]) if os.environ.get("CRT_HIP_LIB") else LIB_DIR / "libcrt_hip.so"
 HOST_LIB = LIB_DIR / "libcrt_host.so"
 
 

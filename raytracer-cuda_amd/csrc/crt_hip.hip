@@ -51,6 +51,10 @@ struct RenderParams {
     int sphere_first, n_ray_spheres;      // variant 4: spheres tested per ray at generation (not in the BVH)
     const float4* __restrict__ sphere_chain;   // their reference scene-level leaf boxes (see ray_spheres)
     int n_chain;                                // boxes in sphere_chain
+    // exactly two per-ray spheres (every reference scene: SceneManager's ground + metal sphere): their data
+    // by value; the kernels stage it in LDS once, so a pass reads it with uniform LDS loads instead of two
+    // dependent vector loads.  Per sphere: center.xyz, radius^2, rank bits, box lo.xyz, box hi.xyz, pad
+    float sph2[2][12];
     unsigned* err;                // device error flag (bit 0: primitive index out of range)
     int width, height, spp, max_bounces;
     int accumulate;
@@ -65,6 +69,7 @@ struct TraceCounts {
     uint32_t boxes, tris, spheres, step_slots, round_slots, trace_calls;
     // COUNT-mode section profile (variant 4; wave-uniform shader-clock cycles, s_memtime)
     uint64_t cyc_regen, cyc_step, cyc_round, passes;
+    uint64_t cyc_shade, cyc_next;   // inside the regen pass: shade(), next_ray(); the rest is ray init
 };
 __device__ __forceinline__ uint64_t shader_clock() { return __builtin_amdgcn_s_memtime(); }
 
@@ -550,11 +555,63 @@ __device__ __forceinline__ bool ref_scene_box(float4 A, float4 B, V3 o, V3 inv) 
     tmax = fminf(tmax, __builtin_inff());
     return !(tmax <= tmin);
 }
+// Sphere::hit's candidate root from its discriminant terms (Sphere.cuh:27-47 with closest = inf).
+__device__ __forceinline__ float sphere_root(float qa, float hb, float disc) {
+    if (disc < 0) return -1.f;
+    const float sq = sqrtf(disc);
+    float root = (-hb - sq) / qa;
+    if (root < 0.001f) {
+        root = (-hb + sq) / qa;
+        if (root < 0.001f) return -1.f;
+    }
+    return root;
+}
+
+// Two spheres at once (data from the kernel arguments): the reference box tests and the discriminant
+// arithmetic in packed f32 (IEEE per half, the reference's operation order: (x*x + y*y) + z*z), roots and
+// divisions per sphere.
+__device__ __forceinline__ void ray_spheres2(const float* sa, const float* sb, V3 o, V3 d, V3 inv,
+                                             float& closest, int& hit) {
+    const pf2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const pf2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+    const pf2 t0x = ((pf2){sa[5], sb[5]} - ox) * ix, t1x = ((pf2){sa[8], sb[8]} - ox) * ix;
+    const pf2 t0y = ((pf2){sa[6], sb[6]} - oy) * iy, t1y = ((pf2){sa[9], sb[9]} - oy) * iy;
+    const pf2 t0z = ((pf2){sa[7], sb[7]} - oz) * iz, t1z = ((pf2){sa[10], sb[10]} - oz) * iz;
+    bool reach[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        float tmin = fmaxf(fmaxf(fminf(t0x[s], t1x[s]), fminf(t0y[s], t1y[s])), fminf(t0z[s], t1z[s]));
+        float tmax = fminf(fminf(fmaxf(t0x[s], t1x[s]), fmaxf(t0y[s], t1y[s])), fmaxf(t0z[s], t1z[s]));
+        tmin = fmaxf(tmin, 0.001f);
+        reach[s] = !(tmax <= tmin);
+    }
+    if (!(reach[0] || reach[1])) return;
+    const pf2 ocx = ox - (pf2){sa[0], sb[0]}, ocy = oy - (pf2){sa[1], sb[1]}, ocz = oz - (pf2){sa[2], sb[2]};
+    const float qa = dot(d, d);
+    const pf2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
+    const pf2 hb = (ocx * dx + ocy * dy) + ocz * dz;
+    const pf2 qc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - (pf2){sa[3], sb[3]};
+    const pf2 qa2 = {qa, qa};
+    const pf2 disc = hb * hb - qa2 * qc;
+    const float ta = reach[0] ? sphere_root(qa, hb.x, disc.x) : -1.f;
+    const float tb = reach[1] ? sphere_root(qa, hb.y, disc.y) : -1.f;
+    const int ra = __float_as_int(sa[4]), rb = __float_as_int(sb[4]);
+    if (ta >= 0.f && better(ta, ra, closest, hit)) { closest = ta; hit = ra; }
+    if (tb >= 0.f && better(tb, rb, closest, hit)) { closest = tb; hit = rb; }
+}
+
+// inv: AABB::hit's 1/d, bit-exact (recip_exact_any), shared with the traversal.
 __device__ __forceinline__ void ray_spheres(const float4* __restrict__ prims, const float4* __restrict__ chain,
-                                            int n_chain, int first, int n, V3 o, V3 d, float& closest, int& hit) {
+                                            int n_chain, int first, int n, V3 o, V3 d, V3 inv, float& closest,
+                                            int& hit, const float* sph2 = nullptr) {
     if (n == 0) return;
-    // AABB::hit's 1/d, bit-exact (rcp + Newton inside its exhaustively verified range, division outside)
-    const V3 inv = v3(recip_exact_any(d.x), recip_exact_any(d.y), recip_exact_any(d.z));
+#ifdef CRT_PROFILE_NO_RAY_SPHERES
+    return;   // profiling build only (tools/build_profile_lib.sh): measures what the per-ray sphere tests cost
+#endif
+    if (n == 2 && sph2) {
+        ray_spheres2(sph2, sph2 + 12, o, d, inv, closest, hit);
+        return;
+    }
     for (int s = 0; s < n; ++s) {
         const int p = first + s;
         const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1];
@@ -582,7 +639,7 @@ __device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     closest = __builtin_inff();
     int hit = -1, node = 0, sp = 0;
-    ray_spheres(prims, chain, n_chain, sphere_first, n_spheres, o, d, closest, hit);
+    ray_spheres(prims, chain, n_chain, sphere_first, n_spheres, o, d, inv, closest, hit);
     int stack[64];
     while (node >= 0) {
         const float4* q = nodes + 8 * (size_t)node;
@@ -875,6 +932,11 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
     // variant 4: 16 LDS stack entries per lane at 5 waves/SIMD; 12 at 6+ so 6 workgroups fit the 160 KiB
     constexpr int SD = VARIANT == 4 ? (MINW >= 6 ? 12 : STACK_LDS) : 1;
     __shared__ uint32_t stack_lds[VARIANT == 4 ? 4 * SD * 64 : 1];
+    __shared__ float sph_lds[24];
+    if (VARIANT == 4) {
+        if (threadIdx.x < 24) sph_lds[threadIdx.x] = (&P.sph2[0][0])[threadIdx.x];
+        __syncthreads();
+    }
     // 16x16 pixel tile per workgroup, 8x8 per wave64.
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -905,7 +967,7 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
     C.lens = Cd.lens_radius;
     C.fw = (float)P.width;
     C.fh = (float)P.height;
-    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
     if (VARIANT == 0) {
         for (;;) {
@@ -936,8 +998,15 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
             if (n_parked >= P.regen_threshold || n_parked == n_live) {
                 if (COUNT) cnt.passes++;
                 if (parked) {
+                    const uint64_t s0 = COUNT ? shader_clock() : 0;
                     if (has_result) shade(S, P, hit, closest);
+                    const uint64_t s1 = COUNT ? shader_clock() : 0;
                     live = next_ray(S, C, x, y, P.max_bounces);
+                    if (COUNT) {
+                        const uint64_t s2 = shader_clock();
+                        cnt.cyc_shade += s1 - s0;
+                        cnt.cyc_next += s2 - s1;
+                    }
                     has_result = false;
                     if (live) {
                         ++S.rays;
@@ -946,9 +1015,11 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
                         sp = 0;
                         closest = INF;
                         hit = -1;
-                        // conservative traversal only needs 1/d to within an ulp (boxes are padded)
-                        inv = v3(__builtin_amdgcn_rcpf(S.d.x), __builtin_amdgcn_rcpf(S.d.y), __builtin_amdgcn_rcpf(S.d.z));
-                        ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d, closest, hit);
+                        // exact 1/d: the per-ray spheres' reference box tests need it (the padded traversal
+                        // would do with rcp)
+                        inv = v3(recip_exact_any(S.d.x), recip_exact_any(S.d.y), recip_exact_any(S.d.z));
+                        ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d, inv,
+                                    closest, hit, sph_lds);
                         if (COUNT) cnt.spheres += P.n_ray_spheres;
                         L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                         if (COUNT) cnt.trace_calls++;
@@ -1041,6 +1112,8 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
             atomicAdd(&P.counters[10], (unsigned long long)cnt.cyc_round);
             atomicAdd(&P.counters[11], (unsigned long long)cnt.passes);
             atomicAdd(&P.counters[12], 1ull);
+            atomicAdd(&P.counters[13], (unsigned long long)cnt.cyc_shade);
+            atomicAdd(&P.counters[14], (unsigned long long)cnt.cyc_next);
         }
     }
     if (lane == 0) atomicAdd(&P.counters[0], (unsigned long long)wr);
@@ -1112,6 +1185,9 @@ __global__ __launch_bounds__(256) void crt_wf_trace_kernel(WfParams W) {
     const RenderParams& P = W.P;
     __shared__ WaveLds lds[4];
     __shared__ uint32_t stack_lds[4 * WF_STACK * 64];
+    __shared__ float sph_lds[24];
+    if (threadIdx.x < 24) sph_lds[threadIdx.x] = (&P.sph2[0][0])[threadIdx.x];
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     WaveLds& L = lds[wave];
@@ -1131,7 +1207,7 @@ __global__ __launch_bounds__(256) void crt_wf_trace_kernel(WfParams W) {
     float4 r0n = make_float4(0.f, 0.f, 0.f, 0.f), r1n = r0n;
     int chunk_next = 0, chunk_end = 0;                     // wave-uniform
     bool more = true;                                      // wave-uniform: the global queue may have entries
-    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     L.owner_at[lane] = 0xff;
     for (;;) {
         if (p < 0 && np >= 0) {                            // swap in the prefetched ray
@@ -1139,12 +1215,13 @@ __global__ __launch_bounds__(256) void crt_wf_trace_kernel(WfParams W) {
             np = -1;
             o = v3(r0n.x, r0n.y, r0n.z);
             d = v3(r0n.w, r1n.x, r1n.y);
-            inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+            inv = v3(recip_exact_any(d.x), recip_exact_any(d.y), recip_exact_any(d.z));
             node = 0;
             sp = 0;
             closest = INF;
             hit = -1;
-            ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, o, d, closest, hit);
+            ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, o, d, inv, closest, hit,
+                        sph_lds);
             if (COUNT) cnt.spheres += P.n_ray_spheres;
             L.ray0[lane] = make_float4(o.x, o.y, o.z, d.x);
         }
@@ -1319,7 +1396,7 @@ __global__ __launch_bounds__(256) void crt_compare_kernel(CompareParams Q) {
     C.lens = Cd.lens_radius;
     C.fw = (float)P.width;
     C.fh = (float)P.height;
-    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long n_rank = 0, n_t = 0, n_bmiss = 0, n_amiss = 0;
     while (next_ray(S, C, x, y, P.max_bounces)) {
         ++S.rays;
@@ -1502,6 +1579,7 @@ const std::vector<uint32_t>& seq_tables() {
 }
 
 inline float i2f(int v) { float f; std::memcpy(&f, &v, 4); return f; }
+inline int i2i_host(float f) { int v; std::memcpy(&v, &f, 4); return v; }
 
 inline bool zero_thickness(const float bmin[3], const float bmax[3]) {
     // AABB::hit can never report such a box (the slab of that axis is empty: tmax <= tmin)
@@ -1854,6 +1932,7 @@ struct crt_scene {
     int width = 2;                 // 2: threaded layouts (variants 0-3); 4: 4-wide nodes (variant 4)
     int stack_cap = 0;             // width 4: traversal-stack entries a ray can need
     int sphere_first = 0, n_ray_spheres = 0;   // width 4: spheres tested per ray, prims [first, first + n)
+    float sph2[2][12] = {};                    // width 4 with exactly two per-ray spheres: their kernel-argument copy
     long excluded = 0;
 };
 
@@ -1871,7 +1950,7 @@ struct crt_renderer {
     bool timed = false;
     int variant = 3;               // see crt_renderer_set_kernel_variant
     unsigned long long diag[3] = {0, 0, 0};
-    unsigned long long prof[5] = {0, 0, 0, 0, 0};   // COUNT-mode section profile (variant 4)
+    unsigned long long prof[7] = {0, 0, 0, 0, 0, 0, 0};   // COUNT-mode section profile (variant 4)
     int regen_threshold = 24;      // variants 2/3
     int regen_threshold_wide = 40; // variant 4 (measured optimum on the 4-wide BVH, profiles/r01d)
     int min_waves = 5;             // variant 2 occupancy target: 1 (compiler's choice), 5, 6 or 8
@@ -2008,6 +2087,16 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
     S->width = rebuilt ? RB.width : 2;
     S->stack_cap = rebuilt ? RB.stack_bound : 0;
     S->sphere_first = rebuilt ? RB.sphere_first : 0;
+    if (rebuilt && RB.n_ray_spheres == 2) {
+        for (int s = 0; s < 2; ++s) {
+            const size_t q = 3 * (size_t)(RB.sphere_first + s);
+            const float4 f0 = RB.prims[q], f1 = RB.prims[q + 1];
+            const int k = i2i_host(f1.w);
+            const float4 A = RB.chain[2 * (size_t)k], B = RB.chain[2 * (size_t)k + 1];
+            const float v[12] = {f0.x, f0.y, f0.z, f1.x, f1.z, A.x, A.y, A.z, A.w, B.x, B.y, 0.f};
+            std::memcpy(S->sph2[s], v, sizeof v);
+        }
+    }
     S->n_chain = rebuilt ? (int)(RB.chain.size() / 2) : 0;
     S->n_ray_spheres = rebuilt ? RB.n_ray_spheres : 0;
     auto up = [&](float4** dst, const std::vector<float4>& src) -> hipError_t {
@@ -2262,6 +2351,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.n_ray_spheres = S->n_ray_spheres;
     P.sphere_chain = S->d_chain;
     P.n_chain = S->n_chain;
+    std::memcpy(P.sph2, S->sph2, sizeof P.sph2);
     P.stack_lds = std::min(R->stack_lds, R->min_waves >= 6 ? 12 : STACK_LDS);
     if (S->width == 4 && S->stack_cap > P.stack_lds) {
         const size_t need = (size_t)(S->stack_cap - P.stack_lds);
@@ -2361,6 +2451,7 @@ int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene*
     }
     P.sphere_first = A->sphere_first; P.n_ray_spheres = A->n_ray_spheres; P.sphere_chain = A->d_chain;
     P.n_chain = A->n_chain;
+    std::memcpy(P.sph2, A->sph2, sizeof P.sph2);
     Q.sphere_first_b = B->sphere_first; Q.n_spheres_b = B->n_ray_spheres; Q.chain_b = B->d_chain;
     Q.n_chain_b = B->n_chain;
     dim3 grid((R->width + 15) / 16, (R->height + 15) / 16), block(256);
@@ -2431,14 +2522,14 @@ int crt_renderer_get_counters(crt_renderer* R, crt_work_counters* out) {
     unsigned long long c[16];
     if (int rc = read_dev(R, c, R->d_counters, sizeof c)) return rc;
     R->diag[0] = c[5]; R->diag[1] = c[6] & ((1ull << 40) - 1); R->diag[2] = c[6] >> 40;
-    for (int i = 0; i < 5; ++i) R->prof[i] = c[8 + i];
+    for (int i = 0; i < 7; ++i) R->prof[i] = c[8 + i];
     out->rays = c[0]; out->box_tests = c[1]; out->tri_tests = c[2]; out->sphere_tests = c[3]; out->paths = c[4];
     if (c[7]) return set_error(CRT_ERR_HIP, "render kernel reported an internal indexing error");
     return CRT_OK;
 }
-int crt_renderer_get_section_profile(crt_renderer* R, unsigned long long* out5) {
-    if (!R || !out5) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
-    for (int i = 0; i < 5; ++i) out5[i] = R->prof[i];
+int crt_renderer_get_section_profile(crt_renderer* R, unsigned long long* out7) {
+    if (!R || !out7) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    for (int i = 0; i < 7; ++i) out7[i] = R->prof[i];
     return CRT_OK;
 }
 int crt_renderer_get_schedule_stats(crt_renderer* R, unsigned long long* out3) {
