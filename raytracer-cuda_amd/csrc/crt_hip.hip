@@ -193,25 +193,28 @@ __device__ __forceinline__ void wave_sync() {
 #define CRT_DPP_ROW_SHR(n) (0x110 | (n))
 #define CRT_DPP_BCAST15 0x142
 #define CRT_DPP_BCAST31 0x143
+// bound_ctrl: a lane whose source is out of range reads 0 (the identity), so LLVM's DPP combiner can fold
+// each step into one v_add_u32_dpp / v_max_u32_dpp instead of v_mov (identity) + v_mov_dpp + the op.
 __device__ __forceinline__ int wave_inclusive_scan(int x, int /*lane*/) {
-    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_ROW_SHR(1), 0xf, 0xf, false);
-    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_ROW_SHR(2), 0xf, 0xf, false);
-    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_ROW_SHR(4), 0xf, 0xf, false);
-    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_ROW_SHR(8), 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_ROW_SHR(1), 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_ROW_SHR(2), 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_ROW_SHR(4), 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_ROW_SHR(8), 0xf, 0xf, true);
     x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_BCAST15, 0xa, 0xf, false);
     x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_BCAST31, 0xc, 0xf, false);
     return x;
 }
-__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
-__device__ __forceinline__ int wave_inclusive_max_scan(int x, int /*lane*/) {
-    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, CRT_DPP_ROW_SHR(1), 0xf, 0xf, false));
-    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, CRT_DPP_ROW_SHR(2), 0xf, 0xf, false));
-    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, CRT_DPP_ROW_SHR(4), 0xf, 0xf, false));
-    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, CRT_DPP_ROW_SHR(8), 0xf, 0xf, false));
-    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, CRT_DPP_BCAST15, 0xa, 0xf, false));
-    x = imax(x, __builtin_amdgcn_update_dpp(-1, x, CRT_DPP_BCAST31, 0xc, 0xf, false));
+// Inclusive max-scan of non-negative values (0 = none) with the same structure.
+__device__ __forceinline__ uint32_t wave_inclusive_max_scan_u(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CRT_DPP_ROW_SHR(1), 0xf, 0xf, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CRT_DPP_ROW_SHR(2), 0xf, 0xf, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CRT_DPP_ROW_SHR(4), 0xf, 0xf, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CRT_DPP_ROW_SHR(8), 0xf, 0xf, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CRT_DPP_BCAST15, 0xa, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CRT_DPP_BCAST31, 0xc, 0xf, false));
     return x;
 }
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
 // Reference (ds_bpermute) form, used by the scan self-test.
 __device__ __forceinline__ int wave_inclusive_scan_shfl(int x, int lane) {
 #pragma unroll
@@ -321,7 +324,7 @@ __device__ int trace_coop(const float4* __restrict__ nodes, const float4* __rest
     int hit = -1;
     int node = active ? 0 : n_nodes;
     L.ray0[lane] = make_float4(o.x, o.y, o.z, d.x);
-    L.owner_at[lane] = 0xff;
+    L.owner_at[lane] = 0;      // owner + 1, 0 = none
     if (COUNT) cnt.trace_calls++;
     while (__ballot(node < n_nodes)) {
         if (COUNT) cnt.step_slots++;        // one traversal step of the wave (x64 lanes)
@@ -364,18 +367,18 @@ __device__ int trace_coop(const float4* __restrict__ nodes, const float4* __rest
             L.prefix[lane] = pfx;
             L.key[lane] = ~0ull;
         }
-        int carry = 0;
+        uint32_t carry = 0;   // owner + 1 of the last pair of the previous round
         for (int base = 0; base < total; base += 64) {
             if (COUNT) cnt.round_slots++;
             // owner of pair (base + lane): lanes whose leaf starts in this round mark their start slot,
             // then an inclusive max-scan over slots (owners are increasing in slot order) fills the gaps;
             // slots before the first start of the round belong to the previous round's last owner.
-            if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)lane;
+            if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)(lane + 1);
             wave_sync();
-            const int mark = L.owner_at[lane];
-            L.owner_at[lane] = 0xff;                  // reset own slot for the next round
-            int owner = wave_inclusive_max_scan(mark == 0xff ? -1 : mark, lane);
-            owner = owner > carry ? owner : carry;
+            const uint32_t mark = L.owner_at[lane];
+            L.owner_at[lane] = 0;                     // reset own slot for the next round
+            const uint32_t owner1 = max(wave_inclusive_max_scan_u(mark), carry);
+            const int owner = (int)owner1 - 1;
             const int j = base + lane;
             if (j < total) {
                 const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
@@ -391,7 +394,7 @@ __device__ int trace_coop(const float4* __restrict__ nodes, const float4* __rest
                     atomicOr(err, 1u);                // indexing bug: report instead of faulting
                 }
             }
-            carry = __builtin_amdgcn_readlane(owner, 63);
+            carry = __builtin_amdgcn_readlane(owner1, 63);
             wave_sync();
         }
         if (leaf_n > 0) {
@@ -461,15 +464,15 @@ __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, 
         L.prefix[lane] = pfx;
         L.key[lane] = ~0ull;
     }
-    int carry = 0;
+    uint32_t carry = 0;   // owner + 1 of the last pair of the previous round
     for (int base = 0; base < total; base += 64) {
         if (COUNT) cnt.round_slots++;
-        if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)lane;
+        if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)(lane + 1);
         wave_sync();
-        const int mark = L.owner_at[lane];
-        L.owner_at[lane] = 0xff;
-        int owner = wave_inclusive_max_scan(mark == 0xff ? -1 : mark, lane);
-        owner = owner > carry ? owner : carry;
+        const uint32_t mark = L.owner_at[lane];
+        L.owner_at[lane] = 0;
+        const uint32_t owner1 = max(wave_inclusive_max_scan_u(mark), carry);
+        const int owner = (int)owner1 - 1;
         const int j = base + lane;
         if (j < total) {
             const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
@@ -485,7 +488,7 @@ __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, 
                 atomicOr(err, 1u);
             }
         }
-        carry = __builtin_amdgcn_readlane(owner, 63);
+        carry = __builtin_amdgcn_readlane(owner1, 63);
         wave_sync();
     }
     if (leaf_n > 0) {
@@ -752,15 +755,15 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         L.prefix[lane] = pfx;
         L.key[lane] = ~0ull;
     }
-    int carry = 0;
+    uint32_t carry = 0;   // owner + 1 of the last pair of the previous round
     for (int base = 0; base < total; base += 64) {
         if (COUNT) cnt.round_slots++;
-        if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)lane;
+        if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)(lane + 1);
         wave_sync();
-        const int mark = L.owner_at[lane];
-        L.owner_at[lane] = 0xff;
-        int owner = wave_inclusive_max_scan(mark == 0xff ? -1 : mark, lane);
-        owner = owner > carry ? owner : carry;
+        const uint32_t mark = L.owner_at[lane];
+        L.owner_at[lane] = 0;
+        const uint32_t owner1 = max(wave_inclusive_max_scan_u(mark), carry);
+        const int owner = (int)owner1 - 1;
         const int j = base + lane;
         if (j < total) {
             const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
@@ -775,7 +778,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
                 atomicOr(P.err, 1u);
             }
         }
-        carry = __builtin_amdgcn_readlane(owner, 63);
+        carry = __builtin_amdgcn_readlane(owner1, 63);
         wave_sync();
     }
     if (leaf_n > 0) {
@@ -988,7 +991,7 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
         int node = -1, sp = 0, hit = -1;
         float closest = INF;
         V3 inv = v3(0.f, 0.f, 0.f);
-        L.owner_at[lane] = 0xff;
+        L.owner_at[lane] = 0;      // traverse_step4: owner + 1, 0 = none
         for (;;) {
             const bool parked = live && node < 0;
             const int n_parked = __popcll(__ballot(parked));
@@ -1041,7 +1044,7 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
         int node = P.n_nodes, hit = -1, nbase = 0;
         float closest = INF;
         V3 inv = v3(0.f, 0.f, 0.f);
-        L.owner_at[lane] = 0xff;
+        L.owner_at[lane] = 0;      // owner + 1, 0 = none
         for (;;) {
             const bool parked = live && node >= P.n_nodes;
             const int n_parked = __popcll(__ballot(parked));
@@ -1208,7 +1211,7 @@ __global__ __launch_bounds__(256) void crt_wf_trace_kernel(WfParams W) {
     int chunk_next = 0, chunk_end = 0;                     // wave-uniform
     bool more = true;                                      // wave-uniform: the global queue may have entries
     TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    L.owner_at[lane] = 0xff;
+    L.owner_at[lane] = 0;      // traverse_step4: owner + 1, 0 = none
     for (;;) {
         if (p < 0 && np >= 0) {                            // swap in the prefetched ray
             p = np;
@@ -1522,7 +1525,8 @@ __global__ __launch_bounds__(64) void crt_selftest_scan_kernel(const int* in, in
     const int x = in[64 * w + lane];
     out[3 * (64 * w + lane)] = wave_inclusive_scan(x, lane);
     out[3 * (64 * w + lane) + 1] = wave_inclusive_scan_shfl(x, lane);
-    out[3 * (64 * w + lane) + 2] = wave_inclusive_max_scan(x, lane);
+    // the kernels' max-scan runs on owner + 1 (0 = none); inputs here are >= -1
+    out[3 * (64 * w + lane) + 2] = (int)wave_inclusive_max_scan_u((uint32_t)(x + 1)) - 1;
 }
 
 __global__ void crt_selftest_rng_kernel(const uint32_t* st_in, int n, int n_draw, float* out) {

@@ -1,5 +1,5 @@
 set -e
-O=gpurun_out/sph3
+O=gpurun_out/dpp2
 mkdir -p $O
 timeout -k 10 600 python3 -m pytest tests -m gpu -x -q > $O/pytest.log 2>&1
 timeout -k 10 500 python3 tools/mismatch_dump.py $O > $O/log 2>&1
