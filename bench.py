@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--bvh", default="rebuilt", choices=["rebuilt", "reference"])
     ap.add_argument("--bvh-width", type=int, default=4, help="rebuilt BVH: 4 (variant 4) or 2 (threaded)")
     ap.add_argument("--leaf-size", type=int, default=4)
-    ap.add_argument("--traversal-cost", type=float, default=3.0)
+    ap.add_argument("--traversal-cost", type=float, default=2.0)
     ap.add_argument("--no-parity", action="store_true", help="skip the reference-BVH parity frame")
     return ap.parse_args()
 

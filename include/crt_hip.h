@@ -171,7 +171,7 @@ typedef struct crt_scene_options {
     int32_t bvh;              /* CRT_BVH_REFERENCE | CRT_BVH_REBUILT */
     int32_t leaf_size;        /* REBUILT: max triangles per leaf, 1..16 (0 = default 4) */
     int32_t layouts;          /* REBUILT: 1 (single left-first order) or 6 (direction-ordered, default) */
-    float traversal_cost;     /* REBUILT: SAH cost of one node step relative to one triangle test (0 = default) */
+    float traversal_cost;     /* REBUILT: SAH cost of one node step relative to one triangle test (0 = default 2) */
     int32_t width;            /* REBUILT: 4 (default) = 4-wide nodes, stack traversal (kernel variant 4);
                                  2 = threaded binary layouts (variants 0-3) */
     int32_t reserved[3];

@@ -49,6 +49,7 @@ struct RenderParams {
     int stack_cap;                        // variant 4: stack entries a ray can need (host bound)
     int stack_lds;                        // variant 4: entries kept in LDS (<= STACK_LDS; rest in ovf)
     int sphere_first, n_ray_spheres;      // variant 4: spheres tested per ray at generation (not in the BVH)
+    int tree_spheres;                     // variant 4: the 4-wide tree's leaves hold spheres too
     const float4* __restrict__ sphere_chain;   // their reference scene-level leaf boxes (see ray_spheres)
     int n_chain;                                // boxes in sphere_chain
     // exactly two per-ray spheres (every reference scene: SceneManager's ground + metal sphere): their data
@@ -278,11 +279,13 @@ __device__ __forceinline__ float sphere_candidate(float4 f0, float4 f1, V3 o, V3
     return root;
 }
 
-// Any primitive of a CRT_BVH_REBUILT leaf: triangle, or sphere (record word 11 == 1).
-__device__ __forceinline__ float prim_test(const float4* __restrict__ prims, int p, V3 o, V3 d, float tmax, int& rank) {
+// Any primitive of a CRT_BVH_REBUILT leaf: triangle, or sphere (record word 11 == 1; only when the tree
+// holds spheres — a uniform flag, so triangle-only trees skip the branch).
+__device__ __forceinline__ float prim_test(const float4* __restrict__ prims, int p, V3 o, V3 d, float tmax, int& rank,
+                                           bool tree_spheres = true) {
     const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1], f2 = prims[3 * p + 2];
     rank = __float_as_int(f2.z);
-    if (__float_as_int(f2.w) == 1) return sphere_candidate(f0, f1, o, d, tmax);
+    if (tree_spheres && __float_as_int(f2.w) == 1) return sphere_candidate(f0, f1, o, d, tmax);
     return tri_test_rec(f0, f1, f2, o, d, tmax);
 }
 
@@ -771,7 +774,8 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
             if (COUNT) cnt.tris++;
             if ((unsigned)p < (unsigned)P.n_prims) {
                 int rank;
-                const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank);
+                const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
+                                          P.tree_spheres != 0);
                 if (t >= 0.f)
                     atomicMin(&L.key[owner], ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank));
             } else {
@@ -1937,6 +1941,7 @@ struct crt_scene {
     int stack_cap = 0;             // width 4: traversal-stack entries a ray can need
     int sphere_first = 0, n_ray_spheres = 0;   // width 4: spheres tested per ray, prims [first, first + n)
     float sph2[2][12] = {};                    // width 4 with exactly two per-ray spheres: their kernel-argument copy
+    int tree_spheres = 1;                      // width 4: some leaf holds a sphere
     long excluded = 0;
 };
 
@@ -2013,7 +2018,7 @@ static int build_scene_arrays(const crt_scene_desc* D, const crt_scene_options* 
     if (o.bvh != CRT_BVH_REFERENCE && o.bvh != CRT_BVH_REBUILT) return set_error(CRT_ERR_INVALID_ARGUMENT, "unknown bvh mode");
     if (o.leaf_size == 0) o.leaf_size = 4;
     if (o.layouts == 0) o.layouts = 6;
-    if (o.traversal_cost == 0.f) o.traversal_cost = 1.f;
+    if (o.traversal_cost == 0.f) o.traversal_cost = 2.f;   // measured optimum for 4-wide leaves <= 4 (profiles/r01i)
     if (o.width == 0) o.width = 4;
     if (o.width != 2 && o.width != 4) return set_error(CRT_ERR_INVALID_ARGUMENT, "width must be 2 or 4");
     if (!(o.traversal_cost > 0.f && o.traversal_cost <= 64.f)) return set_error(CRT_ERR_INVALID_ARGUMENT, "traversal_cost must be in (0, 64]");
@@ -2091,6 +2096,13 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
     S->width = rebuilt ? RB.width : 2;
     S->stack_cap = rebuilt ? RB.stack_bound : 0;
     S->sphere_first = rebuilt ? RB.sphere_first : 0;
+    {
+        int in_tree = 0;   // spheres the 4-wide tree itself holds (not tested per ray)
+        if (rebuilt)
+            for (int r = 0; r < (int)RB.rank_code.size(); ++r)
+                if ((RB.rank_code[r] & SPHERE_BIT) && (RB.rank_code[r] & ~SPHERE_BIT) < RB.sphere_first) ++in_tree;
+        S->tree_spheres = in_tree > 0 || !rebuilt;
+    }
     if (rebuilt && RB.n_ray_spheres == 2) {
         for (int s = 0; s < 2; ++s) {
             const size_t q = 3 * (size_t)(RB.sphere_first + s);
@@ -2355,6 +2367,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.n_ray_spheres = S->n_ray_spheres;
     P.sphere_chain = S->d_chain;
     P.n_chain = S->n_chain;
+    P.tree_spheres = S->tree_spheres;
     std::memcpy(P.sph2, S->sph2, sizeof P.sph2);
     P.stack_lds = std::min(R->stack_lds, R->min_waves >= 6 ? 12 : STACK_LDS);
     if (S->width == 4 && S->stack_cap > P.stack_lds) {

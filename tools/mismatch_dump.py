@@ -15,7 +15,7 @@ out.mkdir(parents=True, exist_ok=True)
 for scene, w, h, spp in (("cornell_bunny", 1280, 720, 32), ("cornell_1m", 1280, 720, 32)):
     hs = crt_amd.HostScene(assets.scene_files(scene))
     ref = hs.upload(0)
-    reb = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=3)
+    reb = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2)
     r = crt_amd.Renderer(w, h)
     r.set_camera(crt_amd.camera(spp))
     r.init_rand(41)
