@@ -34,6 +34,18 @@ namespace crt {
 // CRT_BVH_REBUILT scenes hold 1 or 6 threaded layouts of the same tree back to back (n_nodes each; skip
 // links relative to the layout); internal nodes are NODE_MESH_INNER, leaves as above.
 // materials: 3 x float4 (48 B): (type, albedo.xyz) (emission.xyz, roughness) (ior, 0, 0, 0)
+// shading records: 3 x float4 (48 B) per RANK, everything shade() needs for a hit in one independent pair
+// of loads (instead of rank_code -> prim -> material, three dependent loads):
+//   (a.xyz, kind) (payload) (1/radius, 0, 0, 0)
+//   triangle: a = unit(cross(e1, e2)), the outward normal computed on the host with the device's f32
+//             operation order (Mesh.cuh:303-304; bit-identical); sphere: a = center, kind | SHADE_SPHERE,
+//             outward = (1/radius) * (hp - center) at the hit (Sphere.cuh:44), 1/radius in the third float4
+//   kind & 15 = SHADE_LAMBERT / _METAL / _DIELECTRIC / _LIGHT / _NOEMIT (unknown type: emit 0) /
+//               _INVALID (material index out of range: the same-ray bounce of CUDAKernels.h:127)
+//   payload: lambertian (albedo.xyz, 0)  metal (albedo.xyz, min(roughness, 1))  dielectric (ior, 0, 0, 0)
+//            light (emission.xyz, 0)
+constexpr uint32_t SHADE_LAMBERT = 0, SHADE_METAL = 1, SHADE_DIELECTRIC = 2, SHADE_LIGHT = 3, SHADE_NOEMIT = 4,
+                   SHADE_INVALID = 5, SHADE_SPHERE = 16;
 constexpr int NODE_MESH_INNER = -1;
 constexpr int NODE_SCENE_INNER = -3;
 constexpr int SPHERE_BIT = 1 << 30;

@@ -42,7 +42,7 @@ struct RenderParams {
     const float4* __restrict__ nodes;
     const float4* __restrict__ prims;
     const float4* __restrict__ mats;
-    const int* __restrict__ rank_code;   // reference DFS rank -> prim code (prim index, SPHERE_BIT for spheres)
+    const float4* __restrict__ shade;     // per reference DFS rank: shading record (crt_device.h)
     int n_nodes, n_mats, n_prims;         // n_nodes: nodes of ONE threaded layout
     int n_layouts;                        // 1, or 6 direction-ordered layouts (CRT_BVH_REBUILT)
     uint32_t* __restrict__ ovf;           // variant 4: traversal-stack entries beyond the LDS part
@@ -857,7 +857,8 @@ __device__ __forceinline__ bool next_ray(PathState& S, const CamRegs& C, int x, 
     }
 }
 
-// Phase 3: material scatter / emit / sky (CUDAKernels.h:123-142, Material.cuh:66-146).
+// Phase 3: material scatter / emit / sky (CUDAKernels.h:123-142, Material.cuh:66-146).  The hit's normal and
+// material come from its shading record (crt_device.h): one pair of independent loads per hit.
 __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int hit_rank, float t) {
     if (hit_rank < 0) {                                  // :137-142
         S.pixel = S.pixel + S.thr * sky(S.d);
@@ -865,40 +866,31 @@ __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int h
         S.need_new = true;
         return;
     }
-    const int hit = P.rank_code[hit_rank];
+    const float4* R = P.shade + 3 * (size_t)hit_rank;
+    const float4 r0 = R[0], m = R[1];
+    const uint32_t kind = __float_as_uint(r0.w);
     const V3 hp = S.o + t * S.d;                         // Ray::pointAtDistance
-    V3 outward;
-    uint32_t mat;
-    if (hit >= SPHERE_BIT) {
-        const int p = hit - SPHERE_BIT;
-        const float4 f0 = P.prims[3 * p], f1 = P.prims[3 * p + 1];
-        outward = (1 / f0.w) * (hp - v3(f0.x, f0.y, f0.z));   // Sphere.cuh:44
-        mat = (uint32_t)__float_as_int(f1.y);
-    } else {
-        const float4 f0 = P.prims[3 * hit], f1 = P.prims[3 * hit + 1], f2 = P.prims[3 * hit + 2];
-        outward = unit(cross(v3(f0.w, f1.x, f1.y), v3(f1.z, f1.w, f2.x)));   // Mesh.cuh:303-304
-        mat = (uint32_t)__float_as_int(f2.y);
-    }
+    V3 outward = v3(r0.x, r0.y, r0.z);                   // triangle: unit(cross(e1, e2)), Mesh.cuh:303-304
+    if (kind & SHADE_SPHERE) outward = R[2].x * (hp - outward);   // Sphere.cuh:44: (1 / radius) * (p - center)
     const bool front = dot(S.d, outward) < 0;            // HitInfo::setFaceNormal
     const V3 n = front ? outward : -outward;
-    if (!(mat < (uint32_t)P.n_mats)) {                   // :127 invalid material: same ray again
+    const uint32_t code = kind & 15u;
+    if (code == SHADE_INVALID) {                         // :127 invalid material: same ray again
         ++S.bounce;
         return;
     }
-    const float4 m0 = P.mats[3 * mat], m1 = P.mats[3 * mat + 1];
-    const int mtype = __float_as_int(m0.x);
-    if (mtype == CRT_LAMBERTIAN) {                       // Material.cuh:66-77
+    if (code == SHADE_LAMBERT) {                         // Material.cuh:66-77
         V3 sd = n + rand_unit_vector(S.s);
         if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = n;
-        S.thr = S.thr * v3(m0.y, m0.z, m0.w);
+        S.thr = S.thr * v3(m.x, m.y, m.z);
         S.o = hp;
         S.d = sd;
         ++S.bounce;
-    } else if (mtype == CRT_METAL) {                     // :89-96
+    } else if (code == SHADE_METAL) {                    // :89-96
         V3 refl = reflect(S.d, n);
-        refl = unit(refl) + (m1.w * rand_unit_vector(S.s));
+        refl = unit(refl) + (m.w * rand_unit_vector(S.s));
         if (dot(refl, n) > 0) {
-            S.thr = S.thr * v3(m0.y, m0.z, m0.w);
+            S.thr = S.thr * v3(m.x, m.y, m.z);
             S.o = hp;
             S.d = refl;
             ++S.bounce;
@@ -907,8 +899,8 @@ __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int h
             ++S.paths;
             S.need_new = true;
         }
-    } else if (mtype == CRT_DIELECTRIC) {                // :109-128
-        const float ior = P.mats[3 * mat + 2].x;
+    } else if (code == SHADE_DIELECTRIC) {               // :109-128
+        const float ior = m.x;
         const float ri = front ? (1.0f / ior) : ior;
         const V3 ud = unit(S.d);
         const double cos_theta = fminf(dot(-ud, n), 1.0f);
@@ -923,7 +915,7 @@ __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int h
         S.d = dir;
         ++S.bounce;   // attenuation (1,1,1): thr unchanged (x*1 == x)
     } else {                                             // DiffuseLight: return emit() raw
-        const V3 em = (mtype == CRT_DIFFUSE_LIGHT) ? v3(m1.x, m1.y, m1.z) : v3(0.0f, 0.0f, 0.0f);
+        const V3 em = code == SHADE_LIGHT ? v3(m.x, m.y, m.z) : v3(0.0f, 0.0f, 0.0f);
         S.pixel = S.pixel + em;
         ++S.paths;
         S.need_new = true;
@@ -1933,7 +1925,7 @@ struct crt_scene {
     float4* d_mats = nullptr;
     float4* d_chain = nullptr;     // width 4: reference scene-level boxes on the per-ray spheres' paths
     int n_chain = 0;
-    int* d_rank_code = nullptr;
+    float4* d_shade = nullptr;     // shading record per rank (crt_device.h)
     int n_nodes = 0, n_prims = 0, n_mats = 0, n_ranks = 0;   // n_nodes per layout
     int max_depth = 0;
     int bvh = CRT_BVH_REFERENCE, layouts = 1;
@@ -2066,6 +2058,51 @@ int crt_scene_export(const crt_scene_desc* D, const crt_scene_options* opts, flo
     return CRT_OK;
 }
 
+// Per-rank shading records (layout in crt_device.h).  The triangle normal is unit(cross(e1, e2)) in the
+// device's f32 operation order (the library is compiled with -ffp-contract=off and IEEE sqrt / division on
+// the host too), so the record holds exactly the value shade() used to compute per hit.
+static std::vector<float4> shading_records(const std::vector<int>& rank_code, const std::vector<float4>& prims,
+                                           const crt_scene_desc* D) {
+    std::vector<float4> out(3 * rank_code.size(), make_float4(0.f, 0.f, 0.f, 0.f));
+    for (size_t r = 0; r < rank_code.size(); ++r) {
+        const bool sphere = (rank_code[r] & SPHERE_BIT) != 0;
+        const size_t p = (size_t)(rank_code[r] & ~SPHERE_BIT);
+        const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1], f2 = prims[3 * p + 2];
+        const uint32_t mat = (uint32_t)i2i_host(sphere ? f1.y : f2.y);
+        uint32_t code = SHADE_INVALID;
+        float4 pay = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (mat < (uint32_t)D->n_materials) {
+            const crt_material_desc& M = D->materials[mat];
+            switch (M.type) {
+                case CRT_LAMBERTIAN: code = SHADE_LAMBERT; pay = make_float4(M.albedo[0], M.albedo[1], M.albedo[2], 0.f); break;
+                case CRT_METAL:
+                    code = SHADE_METAL;
+                    pay = make_float4(M.albedo[0], M.albedo[1], M.albedo[2], M.roughness < 1.f ? M.roughness : 1.f);
+                    break;
+                case CRT_DIELECTRIC: code = SHADE_DIELECTRIC; pay = make_float4(M.ior, 0.f, 0.f, 0.f); break;
+                case CRT_DIFFUSE_LIGHT:
+                    code = SHADE_LIGHT;
+                    pay = make_float4(M.emission[0], M.emission[1], M.emission[2], 0.f);
+                    break;
+                default: code = SHADE_NOEMIT; break;
+            }
+        }
+        float4 a;
+        if (sphere) {
+            a = make_float4(f0.x, f0.y, f0.z, i2f((int)(code | SHADE_SPHERE)));
+            out[3 * r + 2] = make_float4(1 / f0.w, 0.f, 0.f, 0.f);
+        } else {
+            const float ux = f0.w, uy = f1.x, uz = f1.y, vx = f1.z, vy = f1.w, vz = f2.x;
+            const float cx = uy * vz - uz * vy, cy = uz * vx - ux * vz, cz = ux * vy - uy * vx;
+            const float s = 1.0f / std::sqrt(cx * cx + cy * cy + cz * cz);
+            a = make_float4(s * cx, s * cy, s * cz, i2f((int)code));
+        }
+        out[3 * r] = a;
+        out[3 * r + 1] = pay;
+    }
+    return out;
+}
+
 int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_options* opts, crt_scene** out) {
     if (!D || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
     *out = nullptr;
@@ -2128,8 +2165,7 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
         (e = up(&S->d_prims, rebuilt ? RB.prims : F.prims)) != hipSuccess ||
         (e = up(&S->d_mats, mats)) != hipSuccess ||
         (e = up(&S->d_chain, rebuilt ? RB.chain : std::vector<float4>())) != hipSuccess ||
-        (e = hipMalloc((void**)&S->d_rank_code, std::max<size_t>(rc.size(), 1) * sizeof(int))) != hipSuccess ||
-        (!rc.empty() && (e = hipMemcpy(S->d_rank_code, rc.data(), rc.size() * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)) {
+        (e = up(&S->d_shade, shading_records(rc, rebuilt ? RB.prims : F.prims, D))) != hipSuccess) {
         crt_scene_destroy(S);
         return set_error(CRT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e));
     }
@@ -2144,7 +2180,7 @@ int crt_scene_get_stats(const crt_scene* S, crt_scene_stats* out) {
     out->stack_bound = S->stack_cap;
     out->device_prims = S->n_prims;
     out->device_bytes = (int64_t)S->n_nodes * S->layouts * (S->width == 4 ? 128 : 32) + (int64_t)S->n_prims * 48 + (int64_t)S->n_mats * 48 +
-                        (int64_t)S->n_ranks * 4;
+                        (int64_t)S->n_ranks * 48;
     out->max_depth = S->max_depth;
     out->n_materials = S->n_mats;
     out->bvh = S->bvh;
@@ -2159,7 +2195,7 @@ void crt_scene_destroy(crt_scene* S) {
     if (S->d_nodes) (void)hipFree(S->d_nodes);
     if (S->d_prims) (void)hipFree(S->d_prims);
     if (S->d_mats) (void)hipFree(S->d_mats);
-    if (S->d_rank_code) (void)hipFree(S->d_rank_code);
+    if (S->d_shade) (void)hipFree(S->d_shade);
     if (S->d_chain) (void)hipFree(S->d_chain);
     delete S;
 }
@@ -2355,7 +2391,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     hipStream_t st = (hipStream_t)stream;
     HIP_TRY(hipMemsetAsync(R->d_counters, 0, 16 * sizeof(unsigned long long), st));
     RenderParams P;
-    P.nodes = S->d_nodes; P.prims = S->d_prims; P.mats = S->d_mats; P.rank_code = S->d_rank_code;
+    P.nodes = S->d_nodes; P.prims = S->d_prims; P.mats = S->d_mats; P.shade = S->d_shade;
     P.n_nodes = S->n_nodes; P.n_mats = S->n_mats; P.n_prims = S->n_prims; P.n_layouts = S->layouts;
     P.err = reinterpret_cast<unsigned*>(R->d_counters + 7);
     P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
@@ -2450,7 +2486,7 @@ int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene*
     HIP_TRY(hipMemset(R->d_counters, 0, 16 * sizeof(unsigned long long)));
     CompareParams Q;
     RenderParams& P = Q.A;
-    P.nodes = A->d_nodes; P.prims = A->d_prims; P.mats = A->d_mats; P.rank_code = A->d_rank_code;
+    P.nodes = A->d_nodes; P.prims = A->d_prims; P.mats = A->d_mats; P.shade = A->d_shade;
     P.n_nodes = A->n_nodes; P.n_mats = A->n_mats; P.n_prims = A->n_prims; P.n_layouts = A->layouts;
     P.err = reinterpret_cast<unsigned*>(R->d_counters + 7);
     P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
