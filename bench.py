@@ -224,7 +224,10 @@ def main():
         r.synchronize()
         work = r.counters()
         assert work["rays"] == rays_rank, "counting kernel disagrees with the timed kernel"
-    variant = 4 if st.get("width") == 4 else (args.kernel_variant if args.kernel_variant is not None else 3)
+    if st.get("width") == 4:
+        variant = 4
+    else:
+        variant = args.kernel_variant if args.kernel_variant is not None else 3
     kname = f"crt_render_kernel<false, {variant}, 5>"
     if work is not None:
         bytes_launch = (B_BOX * work["box_tests"] + B_TRI * work["tri_tests"] + B_SPHERE * work["sphere_tests"]

@@ -215,7 +215,8 @@ int  crt_renderer_set_camera(crt_renderer* r, const crt_camera_desc* cam);
  * regeneration (lanes start their next ray without waiting for the wave's slowest trace); 3 = 2 +
  * next-node prefetch overlapping the leaf rounds.  Scenes with 4-wide nodes (CRT_BVH_REBUILT, width 4)
  * use variant 4 (the variant-3 scheduling over 4-wide nodes with a per-lane stack) unless variant 5 is
- * selected: the wavefront path (trace and shade kernels over a queue of active pixels, same results). */
+ * selected: the wavefront path (trace and shade kernels over a queue of active pixels, same results).
+ * On threaded scenes, variants 4 and 5 run variant 3. */
 int  crt_renderer_set_kernel_variant(crt_renderer* r, int variant);
 /* Variant 5: idle lanes that trigger a queue fetch in the trace kernel (1..64, default 16) and trace/shade
  * iterations between host reads of the queue length (default 16).  Variant-5 renders return after the
@@ -228,7 +229,9 @@ int  crt_renderer_set_regen_threshold(crt_renderer* r, int lanes);
 /* Variant 4: per-lane traversal-stack entries kept in LDS (1..16, default 16); deeper entries spill to a
  * per-pixel region in HBM.  Results do not depend on it (tests force the HBM path with 1). */
 int  crt_renderer_set_stack_lds(crt_renderer* r, int entries);
-/* Variants 2-4: register-allocation occupancy target in waves per SIMD (1 = compiler default, 4-8). */
+/* Variants 2-4: register-allocation occupancy target in waves per SIMD (1 = compiler default, 4-8;
+ * 0 = auto, the default: 6 for 4-wide scenes, 5 otherwise).  At 6+ waves the 4-wide kernel keeps 12
+ * (7: 11) traversal-stack entries per lane in LDS. */
 int  crt_renderer_set_occupancy_target(crt_renderer* r, int waves_per_simd);
 /* Trace `spp` samples per pixel continuing each pixel's RNG stream; the per-pixel
  * linear sum (pixel_color, CUDAKernels.h:157-162) is kept in an fp32 W*H*3 buffer. */

@@ -50,6 +50,26 @@ constexpr int NODE_MESH_INNER = -1;
 constexpr int NODE_SCENE_INNER = -3;
 constexpr int SPHERE_BIT = 1 << 30;
 
+// Correctly rounded 1/x for the Möller–Trumbore determinant: v_rcp_f32 + one FMA Newton step.
+// Exhaustively verified on gfx950 against IEEE division for EVERY float with
+// 1e-8 <= |x| < RCP_FAST_MAX (crt_selftest_rcp, tests/test_gpu_parity.py); outside that range
+// the exact division sequence is used, so the result always equals 1.f / x bit for bit.
+constexpr float RCP_FAST_MAX = 8.507059e37f;   // 2^126: reciprocal stays a normal float
+__device__ __forceinline__ float rcp_newton(float x) {
+    const float r = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+}
+__device__ __forceinline__ float recip_exact(float x) {
+    return fabsf(x) < RCP_FAST_MAX ? rcp_newton(x) : 1.0f / x;
+}
+// 1.f / x for ANY x (the fast path only inside the exhaustively verified range).
+constexpr float RCP_FAST_MIN = 1e-8f;
+__device__ __forceinline__ float recip_exact_any(float x) {
+    const float a = fabsf(x);
+    return (a >= RCP_FAST_MIN && a < RCP_FAST_MAX) ? rcp_newton(x) : 1.0f / x;
+}
+
 struct V3 { float x, y, z; };
 
 __device__ __forceinline__ V3 v3(float a, float b, float c) { return V3{a, b, c}; }
@@ -70,26 +90,6 @@ __device__ __forceinline__ V3 refract(V3 uv, V3 n, float eta) {                 
     V3 perp = eta * (uv + cos_theta * n);
     V3 par = (-sqrtf(fabsf(1.0f - len2(perp)))) * n;
     return perp + par;
-}
-
-// Correctly rounded 1/x for the Möller–Trumbore determinant: v_rcp_f32 + one FMA Newton step.
-// Exhaustively verified on gfx950 against IEEE division for EVERY float with
-// 1e-8 <= |x| < RCP_FAST_MAX (crt_selftest_rcp, tests/test_gpu_parity.py); outside that range
-// the exact division sequence is used, so the result always equals 1.f / x bit for bit.
-constexpr float RCP_FAST_MAX = 8.507059e37f;   // 2^126: reciprocal stays a normal float
-__device__ __forceinline__ float rcp_newton(float x) {
-    const float r = __builtin_amdgcn_rcpf(x);
-    const float e = __builtin_fmaf(-x, r, 1.0f);
-    return __builtin_fmaf(e, r, r);
-}
-__device__ __forceinline__ float recip_exact(float x) {
-    return fabsf(x) < RCP_FAST_MAX ? rcp_newton(x) : 1.0f / x;
-}
-// 1.f / x for ANY x (the fast path only inside the exhaustively verified range).
-constexpr float RCP_FAST_MIN = 1e-8f;
-__device__ __forceinline__ float recip_exact_any(float x) {
-    const float a = fabsf(x);
-    return (a >= RCP_FAST_MIN && a < RCP_FAST_MAX) ? rcp_newton(x) : 1.0f / x;
 }
 
 // ------------------------------------------------------------------ XORWOW

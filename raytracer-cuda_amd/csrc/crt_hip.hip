@@ -71,6 +71,9 @@ struct TraceCounts {
     // COUNT-mode section profile (variant 4; wave-uniform shader-clock cycles, s_memtime)
     uint64_t cyc_regen, cyc_step, cyc_round, passes;
     uint64_t cyc_shade, cyc_next;   // inside the regen pass: shade(), next_ray(); the rest is ray init
+#ifdef CRT_NODE_PREFETCH
+    float pf0 = 0.f, pf1 = 0.f;     // profiling build: one dword per cache line of the lane's next node
+#endif
 };
 __device__ __forceinline__ uint64_t shader_clock() { return __builtin_amdgcn_s_memtime(); }
 
@@ -687,13 +690,19 @@ __device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict
 // takes slot0 and rewrites the entry while slots remain, so the stack holds at most one entry per
 // branching ancestor.  The primitives of the hit leaf children (one consecutive range) join this step's
 // cooperative leaf rounds.  All 64 lanes call it.
+// Overflow stack entry `at` of pixel `pix`: a 32-bit byte offset from the uniform base (the host keeps the
+// region below 4 GiB), so the address is SGPR base + VGPR offset and nothing 64-bit stays live per lane.
+__device__ __forceinline__ uint32_t* ovf_slot(const RenderParams& P, int at, size_t pix, size_t n_pix) {
+    const uint32_t byte = ((uint32_t)(at - P.stack_lds) * (uint32_t)n_pix + (uint32_t)pix) << 2;
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(P.ovf) + byte);
+}
+
 template <bool COUNT>
-__device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d, V3 inv, int& node, int& sp,
-                                               float& closest, int& hit, TraceCounts& cnt, WaveLds& L,
-                                               uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix) {
-    if (COUNT) cnt.step_slots++;
-    const uint64_t c0 = COUNT ? shader_clock() : 0;
-    int leaf_n = 0, leaf_first = 0;
+__device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, int& node, int& sp, float closest,
+                                           TraceCounts& cnt, uint32_t* __restrict__ stk, int lane, size_t pix,
+                                           size_t n_pix, int& leaf_first, int& leaf_n) {
+    leaf_n = 0;
+    leaf_first = 0;
     if (node >= 0) {
         const float4* q = P.nodes + 8 * (size_t)node;
         const float4 mf = q[6];
@@ -724,7 +733,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         cas(k[0], k[1]); cas(k[2], k[3]); cas(k[0], k[2]); cas(k[1], k[3]); cas(k[1], k[2]);
         auto store = [&](int at, uint32_t v) {
             if (at < P.stack_lds) stk[at * 64 + lane] = v;
-            else if (at < P.stack_cap) P.ovf[(size_t)(at - P.stack_lds) * n_pix + pix] = v;
+            else if (at < P.stack_cap) *ovf_slot(P, at, pix, n_pix) = v;
             else atomicOr(P.err, 2u);        // host stack bound violated: report, drop the entry
         };
         if (k[0] != ~0u) {
@@ -738,7 +747,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         } else if (sp > 0) {
             const int at = sp - 1;
             const uint32_t top = at < P.stack_lds ? stk[at * 64 + lane]
-                                                  : (at < P.stack_cap ? P.ovf[(size_t)(at - P.stack_lds) * n_pix + pix] : 0u);
+                                                  : (at < P.stack_cap ? *ovf_slot(P, at, pix, n_pix) : 0u);
             const uint32_t rest = (top >> 6) & 3;
             node = (int)(top >> 8) + (int)((top >> 4) & 3);
             if (rest <= 1) sp = at;
@@ -747,6 +756,23 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
             node = -1;
         }
     }
+#ifdef CRT_NODE_PREFETCH
+    if (node >= 0) {   // touch the next node's two 64 B lines now; the value is never waited on in the loop
+        const float* a = reinterpret_cast<const float*>(P.nodes + 8 * (size_t)node);
+        cnt.pf0 = a[0];
+        cnt.pf1 = a[16];
+    }
+#endif
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d, V3 inv, int& node, int& sp,
+                                               float& closest, int& hit, TraceCounts& cnt, WaveLds& L,
+                                               uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix) {
+    if (COUNT) cnt.step_slots++;
+    const uint64_t c0 = COUNT ? shader_clock() : 0;
+    int leaf_n, leaf_first;
+    node_step4<COUNT>(P, o, inv, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
     const uint64_t c1 = COUNT ? shader_clock() : 0;
     if (COUNT) cnt.cyc_step += c1 - c0;
     if (!__ballot(leaf_n > 0)) return;
@@ -929,16 +955,17 @@ template <bool COUNT, int VARIANT, int MINW>
 __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
     __shared__ WaveLds lds[VARIANT >= 1 ? 4 : 1];
     // variant 4: 16 LDS stack entries per lane at 5 waves/SIMD; 12 at 6+ so 6 workgroups fit the 160 KiB
-    constexpr int SD = VARIANT == 4 ? (MINW >= 6 ? 12 : STACK_LDS) : 1;
-    __shared__ uint32_t stack_lds[VARIANT == 4 ? 4 * SD * 64 : 1];
+    constexpr bool WIDE = VARIANT == 4;
+    constexpr int SD = WIDE ? (MINW >= 7 ? 11 : MINW >= 6 ? 12 : STACK_LDS) : 1;
+    __shared__ uint32_t stack_lds[WIDE ? 4 * SD * 64 : 1];
     __shared__ float sph_lds[24];
-    if (VARIANT == 4) {
+    if (WIDE) {
         if (threadIdx.x < 24) sph_lds[threadIdx.x] = (&P.sph2[0][0])[threadIdx.x];
         __syncthreads();
     }
     // 16x16 pixel tile per workgroup, 8x8 per wave64.
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: LDS bases stay scalar
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
     const bool valid = x < P.width && y < P.height;
@@ -977,7 +1004,7 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
                                          S.d, t, cnt);
             shade(S, P, hit, t);
         }
-    } else if (VARIANT == 4) {
+    } else if (WIDE) {
         // Same scheduling as variant 3 over a 4-wide BVH: node < 0 = no node left (lane parked).
         WaveLds& L = lds[wave];
         uint32_t* stk = stack_lds + wave * SD * 64;
@@ -1016,7 +1043,11 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
                         hit = -1;
                         // exact 1/d: the per-ray spheres' reference box tests need it (the padded traversal
                         // would do with rcp)
+#ifdef CRT_INV_IEEE
+                        inv = v3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
+#else
                         inv = v3(recip_exact_any(S.d.x), recip_exact_any(S.d.y), recip_exact_any(S.d.z));
+#endif
                         ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d, inv,
                                     closest, hit, sph_lds);
                         if (COUNT) cnt.spheres += P.n_ray_spheres;
@@ -1116,6 +1147,9 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
         }
     }
     if (lane == 0) atomicAdd(&P.counters[0], (unsigned long long)wr);
+#ifdef CRT_NODE_PREFETCH
+    if (cnt.pf0 == 1.5e-38f && cnt.pf1 == -1.5e-38f) atomicOr(P.err, 0u);   // keeps the prefetch loads
+#endif
 }
 
 // ------------------------------------------------------------------ wavefront path (variant 5)
@@ -1954,7 +1988,7 @@ struct crt_renderer {
     unsigned long long prof[7] = {0, 0, 0, 0, 0, 0, 0};   // COUNT-mode section profile (variant 4)
     int regen_threshold = 24;      // variants 2/3
     int regen_threshold_wide = 40; // variant 4 (measured optimum on the 4-wide BVH, profiles/r01d)
-    int min_waves = 5;             // variant 2 occupancy target: 1 (compiler's choice), 5, 6 or 8
+    int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 6 for 4-wide scenes, 5 otherwise
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
     size_t ovf_entries = 0;
     int stack_lds = STACK_LDS;     // variant 4: per-lane stack entries kept in LDS
@@ -2279,7 +2313,7 @@ int crt_renderer_set_kernel_variant(crt_renderer* R, int variant) {
 }
 
 int crt_renderer_set_occupancy_target(crt_renderer* R, int waves_per_simd) {
-    if (!R || waves_per_simd < 1 || waves_per_simd > 8) return set_error(CRT_ERR_INVALID_ARGUMENT, "waves per SIMD 1..8");
+    if (!R || waves_per_simd < 0 || waves_per_simd > 8) return set_error(CRT_ERR_INVALID_ARGUMENT, "waves per SIMD 0..8");
     R->min_waves = waves_per_simd;
     return CRT_OK;
 }
@@ -2405,9 +2439,12 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.n_chain = S->n_chain;
     P.tree_spheres = S->tree_spheres;
     std::memcpy(P.sph2, S->sph2, sizeof P.sph2);
-    P.stack_lds = std::min(R->stack_lds, R->min_waves >= 6 ? 12 : STACK_LDS);
+    const int occ = R->min_waves ? R->min_waves : (S->width == 4 ? 6 : 5);
+    P.stack_lds = std::min(R->stack_lds, occ >= 7 ? 11 : occ >= 6 ? 12 : STACK_LDS);
     if (S->width == 4 && S->stack_cap > P.stack_lds) {
         const size_t need = (size_t)(S->stack_cap - P.stack_lds);
+        if (need * R->width * R->height * 4 >= ((size_t)1 << 32))
+            return set_error(CRT_ERR_INVALID_ARGUMENT, "traversal-stack overflow region would exceed 4 GiB");
         if (need > R->ovf_entries) {         // grow the overflow stack region (rarely needed)
             HIP_TRY(hipStreamSynchronize(st));
             if (R->d_ovf) (void)hipFree(R->d_ovf);
@@ -2425,6 +2462,8 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         P.stack_lds = std::min(R->stack_lds, WF_STACK);
         if (S->stack_cap > P.stack_lds) {
             const size_t need = (size_t)(S->stack_cap - P.stack_lds);
+            if (need * R->width * R->height * 4 >= ((size_t)1 << 32))
+                return set_error(CRT_ERR_INVALID_ARGUMENT, "traversal-stack overflow region would exceed 4 GiB");
             if (need > R->ovf_entries) {
                 HIP_TRY(hipStreamSynchronize(st));
                 if (R->d_ovf) (void)hipFree(R->d_ovf);
@@ -2444,21 +2483,22 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         else hipLaunchKernelGGL((crt_render_kernel<false, V, W>), grid, block, 0, st, P);     \
     } while (0)
     if (S->width == 4) {
-        if (R->min_waves >= 6) CRT_LAUNCH(4, 6);
-        else if (R->min_waves >= 5) CRT_LAUNCH(4, 5);
-        else if (R->min_waves >= 4) CRT_LAUNCH(4, 4);
+        if (occ >= 7) CRT_LAUNCH(4, 7);
+        else if (occ >= 6) CRT_LAUNCH(4, 6);
+        else if (occ >= 5) CRT_LAUNCH(4, 5);
+        else if (occ >= 4) CRT_LAUNCH(4, 4);
         else CRT_LAUNCH(4, 1);
     }
     else if (R->variant == 0) CRT_LAUNCH(0, 1);
     else if (R->variant == 1) CRT_LAUNCH(1, 1);
-    else if (R->variant == 3) {
-        if (R->min_waves >= 5) CRT_LAUNCH(3, 5);
-        else if (R->min_waves >= 4) CRT_LAUNCH(3, 4);
+    else if (R->variant >= 3) {   // 4-5 on a threaded (width-2) scene: its best kernel, variant 3
+        if (occ >= 5) CRT_LAUNCH(3, 5);
+        else if (occ >= 4) CRT_LAUNCH(3, 4);
         else CRT_LAUNCH(3, 1);
     }
-    else if (R->min_waves >= 8) CRT_LAUNCH(2, 8);
-    else if (R->min_waves >= 6) CRT_LAUNCH(2, 6);
-    else if (R->min_waves >= 5) CRT_LAUNCH(2, 5);
+    else if (occ >= 8) CRT_LAUNCH(2, 8);
+    else if (occ >= 6) CRT_LAUNCH(2, 6);
+    else if (occ >= 5) CRT_LAUNCH(2, 5);
     else CRT_LAUNCH(2, 1);
 #undef CRT_LAUNCH
     HIP_TRY(hipGetLastError());

@@ -166,3 +166,4 @@ def test_wavefront_equals_megakernel(rebuilt, refill):
     c.synchronize()
     assert np.array_equal(a.linear().view(np.uint32), c.linear().view(np.uint32))
     assert c.counters()["rays"] == a.counters()["rays"]
+

@@ -66,7 +66,7 @@ print(json.dumps({"config": "reference", "scene": a.scene, "stats": ref.stats(),
 for cfg in a.configs.split(","):
         f = {p[0]: p[1:] for p in cfg.split(":")}
         width, leaf, trav = int(f.get("w", 4)), int(f.get("l", 4)), float(f.get("t", 1))
-        layouts, occ = int(f.get("L", 6 if width == 2 else 1)), int(f.get("o", 5))
+        layouts, occ = int(f.get("L", 6 if width == 2 else 1)), int(f.get("o", 0))
         r.set_occupancy_target(occ)
         r.set_regen_threshold(int(f.get("T", 24)))
         r.set_kernel_variant(int(f.get("V", 3)))
@@ -94,6 +94,6 @@ for cfg in a.configs.split(","):
                                       frac_round=round(prof["cyc_round"] / tot, 3))
         print(json.dumps(out), flush=True)
         sc.close()
-        r.set_occupancy_target(5)
+        r.set_occupancy_target(0)
         r.set_regen_threshold(24)
         r.set_kernel_variant(3)
