@@ -205,6 +205,7 @@ def main():
     kernel_ms_avg = sum(kernel_ms) / len(kernel_ms)
     kernel_ms_max = allreduce_max(max(kernel_ms))
     rays_rank = r.counters()["rays"]
+    kname = r.last_kernel_name()      # the instantiation the timed frames ran (rocprofv3's spelling)
     [rays_frame] = allreduce_sum_i([rays_rank])
     log_r(f"[timed] {args.steps} frames in {elapsed:.3f}s; render kernel {kernel_ms_avg:.1f} ms avg (rank 0); "
           f"{rays_frame} rays/frame")
@@ -228,7 +229,6 @@ def main():
         variant = 4
     else:
         variant = args.kernel_variant if args.kernel_variant is not None else 3
-    kname = f"crt_render_kernel<false, {variant}, 5>"
     if work is not None:
         bytes_launch = (B_BOX * work["box_tests"] + B_TRI * work["tri_tests"] + B_SPHERE * work["sphere_tests"]
                         + B_RAY * work["rays"] + B_PIXEL * W * H)

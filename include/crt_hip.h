@@ -158,8 +158,8 @@ int crt_device_count(int* out);
 /* Acceleration structure the device scene is traversed with.
  *   CRT_BVH_REFERENCE — the reference's own scene + mesh BVHs, flattened unchanged (default).  Bit-exact:
  *     same boxes, same visiting order, same culling, same work counters as BVHNode::hit / Mesh::hit.
- *   CRT_BVH_REBUILT   — a binned-SAH BVH over the same primitives with small padded leaves, emitted in
- *     six direction-ordered threaded layouts (one per dominant ray axis and sign).  Same hit rule as the
+ *   CRT_BVH_REBUILT   — a binned-SAH BVH over the same primitives with small padded leaves, collapsed to
+ *     4-wide nodes (default; width 2 = threaded binary layouts).  Same hit rule as the
  *     reference: closest t in [0.001, closest], ties to the primitive the reference visits LAST
  *     (every primitive carries its reference DFS rank), primitives the reference can never reach
  *     (inside a zero-thickness box) excluded.  Results differ from the reference only where the
@@ -262,6 +262,9 @@ uint8_t* crt_renderer_rgba_device_ptr(crt_renderer* r);
 uint32_t* crt_renderer_rng_device_ptr(crt_renderer* r);
 /* Milliseconds of the last render kernel launch(es), measured with HIP events on the launch stream. */
 float crt_renderer_last_kernel_ms(crt_renderer* r);
+/* Template instantiation of the last render-kernel launch as rocprofv3 names it, e.g.
+ * "crt_render_kernel<false, 4, 6>" (empty before the first launch and for variant 5). */
+const char* crt_renderer_last_kernel_name(const crt_renderer* r);
 
 /* ---- self-test of the arithmetic the kernel depends on (IEEE f32/f64 div/sqrt) ---- */
 /* For n inputs a[i], b[i] (f32) computes on the device: a/b, sqrtf(|a|), 1/a, (double)sqrt((double)|a|)

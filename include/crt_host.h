@@ -42,6 +42,17 @@ int crth_scene_loader_arrays(const crth_scene* s, float* positions, uint32_t* in
 int crth_camera(float aspect, float vfov, const float* pos3, const float* up3, float aperture, float focus,
                 float yaw, float pitch, int spp, crt_camera_desc* out);
 
+/* ---- frame output (WindowManager::drawFrame, WindowManager.h:79-93, headless) ----
+ * rgba: W*H*4 bytes as the renderer holds them (row 0 = bottom).  flip != 0 writes the top row first, as
+ * the window shows it (flipVertically).  Files are 8-bit RGB. */
+#define CRTH_IMAGE_PPM 0
+#define CRTH_IMAGE_PNG 1
+/* Encode into out[*size]; on entry *size is the capacity (out may be NULL to query), on return the
+ * encoded length.  Returns CRT_ERR_INVALID_ARGUMENT (with *size set) when the capacity is too small. */
+int crth_encode_image(int format, const uint8_t* rgba, int width, int height, int flip, uint8_t* out, uint64_t* size);
+/* Write .png or .ppm by the path's extension. */
+int crth_write_image(const char* path, const uint8_t* rgba, int width, int height, int flip);
+
 const char* crth_last_error(void);
 
 #ifdef __cplusplus

@@ -264,6 +264,9 @@ class Renderer:
         return dict(zip(("cyc_regen", "cyc_step", "cyc_round", "passes", "waves", "cyc_shade", "cyc_next"),
                         (int(v) for v in a)))
 
+    def last_kernel_name(self) -> str:
+        return (_lib.hip().crt_renderer_last_kernel_name(self.h) or b"").decode()
+
     def last_kernel_ms(self) -> float:
         return float(_lib.hip().crt_renderer_last_kernel_ms(self.h))
 
@@ -312,3 +315,30 @@ def device_count() -> int:
     n = C.c_int(0)
     check(_lib.hip().crt_device_count(C.byref(n)), "device_count")
     return n.value
+
+
+IMAGE_FORMATS = {"ppm": 0, "png": 1}
+
+
+def encode_image(rgba: np.ndarray, fmt: str = "png", flip: bool = True) -> bytes:
+    """PNG/PPM bytes of an (H, W, 4) uint8 framebuffer (row 0 = bottom, as the renderer holds it);
+    flip=True writes the top row first, like WindowManager::drawFrame (WindowManager.h:79-93)."""
+    a = np.ascontiguousarray(rgba, np.uint8)
+    if a.ndim != 3 or a.shape[2] != 4:
+        raise CrtError("rgba must be (H, W, 4) uint8")
+    h, w = a.shape[:2]
+    n = C.c_uint64(0)
+    L = _lib.host()
+    check_host(L.crth_encode_image(IMAGE_FORMATS[fmt], _p(a), w, h, int(flip), None, C.byref(n)), "crth_encode_image")
+    out = np.empty(n.value, np.uint8)
+    check_host(L.crth_encode_image(IMAGE_FORMATS[fmt], _p(a), w, h, int(flip), _p(out), C.byref(n)), "crth_encode_image")
+    return out[: n.value].tobytes()
+
+
+def write_image(path: str, rgba: np.ndarray, flip: bool = True) -> None:
+    """Write .png / .ppm by extension (crth_write_image)."""
+    a = np.ascontiguousarray(rgba, np.uint8)
+    if a.ndim != 3 or a.shape[2] != 4:
+        raise CrtError("rgba must be (H, W, 4) uint8")
+    check_host(_lib.host().crth_write_image(str(path).encode(), _p(a), a.shape[1], a.shape[0], int(flip)),
+               "crth_write_image")

@@ -83,13 +83,14 @@ HIP_SYMBOLS = [
     "crt_renderer_synchronize", "crt_renderer_read_linear", "crt_renderer_read_rgba8", "crt_renderer_read_rng",
     "crt_renderer_write_linear", "crt_renderer_get_counters", "crt_renderer_linear_device_ptr",
     "crt_renderer_rgba_device_ptr", "crt_renderer_rng_device_ptr", "crt_renderer_last_kernel_ms",
+    "crt_renderer_last_kernel_name",
     "crt_renderer_attach_linear", "crt_renderer_set_kernel_variant", "crt_renderer_get_schedule_stats",
     "crt_renderer_set_regen_threshold", "crt_renderer_set_occupancy_target",
     "crt_selftest_math", "crt_selftest_rng", "crt_selftest_scan", "crt_selftest_rcp",
 ]
 HOST_SYMBOLS = [
     "crth_scene_load", "crth_scene_destroy", "crth_scene_desc", "crth_scene_upload", "crth_scene_upload_ex", "crth_scene_counts",
-    "crth_scene_loader_arrays", "crth_camera", "crth_last_error",
+    "crth_scene_loader_arrays", "crth_camera", "crth_last_error", "crth_encode_image", "crth_write_image",
 ]
 
 _hip = None
@@ -140,6 +141,7 @@ def hip():
             "crt_renderer_get_counters": ([P, P], i32),
             "crt_renderer_linear_device_ptr": ([P], P), "crt_renderer_rgba_device_ptr": ([P], P),
             "crt_renderer_rng_device_ptr": ([P], P), "crt_renderer_last_kernel_ms": ([P], f32),
+            "crt_renderer_last_kernel_name": ([P], C.c_char_p),
             "crt_renderer_attach_linear": ([P, P], i32),
             "crt_renderer_set_kernel_variant": ([P, i32], i32),
             "crt_renderer_get_schedule_stats": ([P, P], i32),
@@ -173,6 +175,8 @@ def host():
             "crth_scene_counts": ([P, P], i32), "crth_scene_loader_arrays": ([P, P, P, P, P, P], i32),
             "crth_camera": ([f32, f32, P, P, f32, f32, f32, f32, i32, P], i32),
             "crth_last_error": ([], C.c_char_p),
+            "crth_encode_image": ([i32, P, i32, i32, i32, P, P], i32),
+            "crth_write_image": ([C.c_char_p, P, i32, i32, i32], i32),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)

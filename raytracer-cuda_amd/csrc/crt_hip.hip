@@ -1983,6 +1983,7 @@ struct crt_renderer {
     bool has_camera = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    char kernel_name[64] = "";     // instantiation of the last render launch, rocprof's spelling
     int variant = 3;               // see crt_renderer_set_kernel_variant
     unsigned long long diag[3] = {0, 0, 0};
     unsigned long long prof[7] = {0, 0, 0, 0, 0, 0, 0};   // COUNT-mode section profile (variant 4)
@@ -2479,6 +2480,8 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     HIP_TRY(hipEventRecord(R->ev0, st));
 #define CRT_LAUNCH(V, W)                                                                     \
     do {                                                                                     \
+        std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, %d, %d>", \
+                      cnt ? "true" : "false", V, W);                                         \
         if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, V, W>), grid, block, 0, st, P);  \
         else hipLaunchKernelGGL((crt_render_kernel<false, V, W>), grid, block, 0, st, P);     \
     } while (0)
@@ -2634,6 +2637,8 @@ int crt_renderer_get_schedule_stats(crt_renderer* R, unsigned long long* out3) {
 float* crt_renderer_linear_device_ptr(crt_renderer* R) { return R ? R->d_sum : nullptr; }
 uint8_t* crt_renderer_rgba_device_ptr(crt_renderer* R) { return R ? R->d_rgba : nullptr; }
 uint32_t* crt_renderer_rng_device_ptr(crt_renderer* R) { return R ? R->d_rng : nullptr; }
+
+const char* crt_renderer_last_kernel_name(const crt_renderer* R) { return R ? R->kernel_name : ""; }
 
 float crt_renderer_last_kernel_ms(crt_renderer* R) {
     if (!R || !R->timed) return -1.f;

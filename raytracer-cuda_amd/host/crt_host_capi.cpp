@@ -4,6 +4,7 @@
 #include <string>
 
 #include "crt/Camera.h"
+#include "crt/ImageIO.h"
 #include "crt/SceneManager.h"
 #include "crt_host.h"
 
@@ -112,6 +113,37 @@ int crth_camera(float aspect, float vfov, const float* pos3, const float* up3, f
     cam.setSamplesPerPixel(spp);
     *out = cam.toDesc();
     return CRT_OK;
+}
+
+int crth_encode_image(int format, const uint8_t* rgba, int w, int h, int flip, uint8_t* out, uint64_t* size) {
+    if (!rgba || !size || w <= 0 || h <= 0 || (format != CRTH_IMAGE_PPM && format != CRTH_IMAGE_PNG)) {
+        g_err = "bad argument";
+        return CRT_ERR_INVALID_ARGUMENT;
+    }
+    try {
+        const std::vector<uint8_t> bytes = format == CRTH_IMAGE_PNG ? CRT::encodePNG(rgba, w, h, flip != 0)
+                                                                    : CRT::encodePPM(rgba, w, h, flip != 0);
+        const uint64_t cap = *size;
+        *size = bytes.size();
+        if (!out) return CRT_OK;
+        if (cap < bytes.size()) { g_err = "output buffer too small"; return CRT_ERR_INVALID_ARGUMENT; }
+        std::memcpy(out, bytes.data(), bytes.size());
+        return CRT_OK;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return CRT_ERR_INVALID_ARGUMENT;
+    }
+}
+
+int crth_write_image(const char* path, const uint8_t* rgba, int w, int h, int flip) {
+    if (!path) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    try {
+        CRT::writeImage(path, rgba, w, h, flip != 0);
+        return CRT_OK;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return CRT_ERR_INVALID_ARGUMENT;
+    }
 }
 
 }  // extern "C"
