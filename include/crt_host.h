@@ -42,6 +42,55 @@ int crth_scene_loader_arrays(const crth_scene* s, float* positions, uint32_t* in
 int crth_camera(float aspect, float vfov, const float* pos3, const float* up3, float aperture, float focus,
                 float yaw, float pitch, int spp, crt_camera_desc* out);
 
+/* ---- interactive loop (Raytracer.h:52-102, Camera.cuh:46-157), headless ----
+ * The reference polls SFML each frame; here the caller passes what it would have polled. */
+#define CRTH_KEY_W        1u
+#define CRTH_KEY_A        2u
+#define CRTH_KEY_S        4u
+#define CRTH_KEY_D        8u
+#define CRTH_KEY_SPACE    16u
+#define CRTH_KEY_LCONTROL 32u
+#define CRTH_KEY_F        64u   /* held: toggles high-quality mode (2000 spp) every frame, like isKeyPressed(F) */
+typedef struct crth_input {
+    float mouse_x, mouse_y;   /* sf::Mouse::getPosition(window) */
+    int32_t right_mouse;      /* isRightMousePressed (rotation while held) */
+    uint32_t keys;            /* CRTH_KEY_* held this frame */
+    int32_t focus_steps;      /* PageUp (+1) / PageDown (-1) presses this frame: adjustFocusDistance(+-0.1) */
+} crth_input;
+
+/* Host-only camera controller: CRT::Camera(aspect, vfov, pos, target(ignored), up, aperture, focus) driven by
+ * Camera::updateCamera(dt, w, h, input).  No GPU needed. */
+typedef struct crth_camera_ctl crth_camera_ctl;
+int  crth_camera_create(float aspect, float vfov, const float* pos3, const float* up3, float aperture, float focus,
+                        crth_camera_ctl** out);
+int  crth_camera_update(crth_camera_ctl* c, float dt, int window_width, int window_height, const crth_input* in);
+/* state: yaw, pitch, moving, rotating, high_quality, focus (6 floats; flags as 0/1) */
+int  crth_camera_get(const crth_camera_ctl* c, crt_camera_desc* desc, float* state6);
+void crth_camera_destroy(crth_camera_ctl* c);
+
+typedef struct crth_frame_info {
+    int64_t frame;            /* frames rendered so far, this one included */
+    int32_t spp;              /* samples traced this frame */
+    int32_t accumulated;      /* samples in the displayed image */
+    int32_t moving, high_quality;
+    float kernel_ms;          /* render kernel (HIP events) */
+    double frame_ms;          /* updateAndRender wall clock, synchronous */
+} crth_frame_info;
+
+/* Raytracer(width, height, aspect, vfov, aperture) over a loaded scene: uploads it to `device` with `opts`
+ * (NULL = CRT_BVH_REFERENCE) and seeds every pixel's RNG (curand_init(seed, pixel, 0)).  pos3 NULL = the
+ * reference's (0,4,4); focus <= 0 = |pos|.  accumulate != 0: still 1-spp frames add up (see Raytracer.h). */
+typedef struct crth_viewer crth_viewer;
+int  crth_viewer_create(const char* const* obj_files, int n_files, int device, const crt_scene_options* opts,
+                        int width, int height, float aspect, float vfov, float aperture, const float* pos3,
+                        float focus, unsigned long long seed, int accumulate, crth_viewer** out);
+/* One frame: Raytracer::updateAndRender(dt, input); info may be NULL. */
+int  crth_viewer_frame(crth_viewer* v, float dt, const crth_input* in, crth_frame_info* info);
+int  crth_viewer_camera(const crth_viewer* v, crt_camera_desc* out);
+/* The viewer's renderer (read_rgba8 / read_linear / read_rng / device pointers via crt_hip.h). */
+crt_renderer* crth_viewer_renderer(crth_viewer* v);
+void crth_viewer_destroy(crth_viewer* v);
+
 /* ---- frame output (WindowManager::drawFrame, WindowManager.h:79-93, headless) ----
  * rgba: W*H*4 bytes as the renderer holds them (row 0 = bottom).  flip != 0 writes the top row first, as
  * the window shows it (flipVertically).  Files are 8-bit RGB. */

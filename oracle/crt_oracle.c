@@ -781,6 +781,7 @@ EXPORT void oracle_camera(float aspect, float vfov, const float* pos3, const flo
 typedef struct {
     const Scene* sc; Cam cam; int w, h, spp, bounces; unsigned long long seed, subseq_base;
     int x0, y0, x1, y1;
+    uint32_t* rng;   /* optional per-pixel XORWOW state (w*h*6: v[5], d), continued and stored back */
     float* sum; unsigned char* rgba; float scale;
     int next_row; pthread_mutex_t mu; Counters total;
 } Job;
@@ -796,12 +797,15 @@ static void* worker(void* arg) {
         if (y >= j->y1) break;
         for (int x = j->x0; x < j->x1; x++) {                         /* CUDAKernels.h:147-166 */
             int pixel = y * j->w + x;
-            Rng s; rng_init(&s, j->seed, j->subseq_base + (unsigned long long)pixel);
+            Rng s;
+            if (j->rng) memcpy(&s, j->rng + 6 * (size_t)pixel, sizeof s);   /* state persists (CUDAKernels.h:151,165) */
+            else rng_init(&s, j->seed, j->subseq_base + (unsigned long long)pixel);
             V3 pc = v3(0, 0, 0);
             for (int smp = 0; smp < j->spp; smp++) {
                 Ray r = cam_get_ray(&j->cam, x, y, j->w, j->h, &s);
                 pc = vadd(pc, ray_color(j->sc, r, j->bounces, &s, &cn));
             }
+            if (j->rng) memcpy(j->rng + 6 * (size_t)pixel, &s, sizeof s);
             size_t o = (size_t)(y - j->y0) * rw + (x - j->x0);
             if (j->sum) { j->sum[3 * o] = pc.e[0]; j->sum[3 * o + 1] = pc.e[1]; j->sum[3 * o + 2] = pc.e[2]; }
             if (j->rgba) {
@@ -824,16 +828,16 @@ static void* worker(void* arg) {
  * oracle_camera.  sum_out: (y1-y0)*(x1-x0)*3 linear sums (pixel_color before
  * m_PixelSampleScale); rgba_out: writeColor(scale * sum) with scale = 1.f/spp_total.
  * counters_out (4 u64): rays, box tests, triangle tests, sphere tests. */
-EXPORT int oracle_render(void* scene, const float* cam19, int w, int h, int spp, int spp_total, int max_bounces,
-                         unsigned long long seed, unsigned long long subseq_base, int x0, int y0, int x1, int y1,
-                         int nthreads, float* sum_out, unsigned char* rgba_out, unsigned long long* counters_out) {
+static int render_job(void* scene, const float* cam19, int w, int h, int spp, int spp_total, int max_bounces,
+                      unsigned long long seed, unsigned long long subseq_base, uint32_t* rng, int x0, int y0, int x1,
+                      int y1, int nthreads, float* sum_out, unsigned char* rgba_out, unsigned long long* counters_out) {
     build_seq_tables();
     Job j; memset(&j, 0, sizeof j);
     j.sc = (const Scene*)scene;
     memcpy(j.cam.pos.e, cam19, 12); memcpy(j.cam.llc.e, cam19 + 3, 12); memcpy(j.cam.horiz.e, cam19 + 6, 12);
     memcpy(j.cam.vert.e, cam19 + 9, 12); memcpy(j.cam.right.e, cam19 + 12, 12); memcpy(j.cam.up.e, cam19 + 15, 12);
     j.cam.lens_r = cam19[18];
-    j.w = w; j.h = h; j.spp = spp; j.bounces = max_bounces; j.seed = seed; j.subseq_base = subseq_base;
+    j.w = w; j.h = h; j.spp = spp; j.bounces = max_bounces; j.seed = seed; j.subseq_base = subseq_base; j.rng = rng;
     j.x0 = x0; j.y0 = y0; j.x1 = x1; j.y1 = y1; j.sum = sum_out; j.rgba = rgba_out;
     j.scale = 1.f / (float)spp_total;                                   /* Camera.cuh:23,71 */
     j.next_row = y0;
@@ -849,4 +853,105 @@ EXPORT int oracle_render(void* scene, const float* cam19, int w, int h, int spp,
         counters_out[2] = j.total.tris; counters_out[3] = j.total.spheres;
     }
     return 0;
+}
+
+EXPORT int oracle_render(void* scene, const float* cam19, int w, int h, int spp, int spp_total, int max_bounces,
+                         unsigned long long seed, unsigned long long subseq_base, int x0, int y0, int x1, int y1,
+                         int nthreads, float* sum_out, unsigned char* rgba_out, unsigned long long* counters_out) {
+    return render_job(scene, cam19, w, h, spp, spp_total, max_bounces, seed, subseq_base, NULL, x0, y0, x1, y1,
+                      nthreads, sum_out, rgba_out, counters_out);
+}
+
+/* One frame of the reference's render loop over persistent RNG state: rng (w*h*6 words: v[5], d per
+ * pixel, from oracle_rng_init or a previous frame) is continued and stored back, like the curandState
+ * array across CUDARenderer::render calls (CUDAKernels.h:151, :165).  Full frame. */
+EXPORT int oracle_render_rng(void* scene, const float* cam19, int w, int h, int spp, int spp_total, int max_bounces,
+                             uint32_t* rng, int nthreads, float* sum_out, unsigned char* rgba_out,
+                             unsigned long long* counters_out) {
+    return render_job(scene, cam19, w, h, spp, spp_total, max_bounces, 0, 0, rng, 0, 0, w, h, nthreads, sum_out,
+                      rgba_out, counters_out);
+}
+
+/* ---- Camera::updateCamera (Camera.cuh:46-157): the per-frame camera controller ----
+ * Input = what the reference polls from SFML: mouse position, right button, keys held
+ * (bits W=1 A=2 S=4 D=8 Space=16 LControl=32 F=64) and PageUp/PageDown presses (focus_steps,
+ * WindowManager.h:64-67).  updateRotation's function-local statics are fields here. */
+typedef struct {
+    Cam c;
+    int spp; float scale;
+    int moves, rotates, hq;
+    int rot_init, first_mouse;
+    float last_x, last_y, smooth_x, smooth_y;
+} CamCtl;
+
+EXPORT void* oracle_camctl_new(float aspect, float vfov, const float* pos3, const float* up3, float aperture,
+                               float focus) {
+    CamCtl* k = (CamCtl*)calloc(1, sizeof(CamCtl));
+    k->c.aspect = aspect; k->c.vfov = vfov; k->c.pos = v3(pos3[0], pos3[1], pos3[2]);
+    k->c.aperture = aperture; k->c.focus = focus; k->c.world_up = v3(up3[0], up3[1], up3[2]);
+    k->c.yaw = -90.0f; k->c.pitch = 0.0f;                                 /* Camera.cuh:18-30 */
+    cam_update(&k->c);
+    k->spp = 1; k->scale = 1.0f / 1;
+    k->first_mouse = 1;
+    return k;
+}
+
+EXPORT void oracle_camctl_free(void* p) { free(p); }
+
+EXPORT void oracle_camctl_update(void* p, float dt, int ww, int wh, float mx, float my, int rmb, unsigned keys,
+                                 int focus_steps) {
+    CamCtl* k = (CamCtl*)p;
+    Cam* c = &k->c;
+    for (int i = 0; i < focus_steps; i++) { c->focus = fmaxf(0.1f, c->focus + 0.1f); cam_update(c); }   /* :79-83 */
+    for (int i = 0; i > focus_steps; i--) { c->focus = fmaxf(0.1f, c->focus + -0.1f); cam_update(c); }
+    /* updateRotation (:88-130) */
+    if (!k->rot_init) {
+        k->last_x = ww / 2.0f; k->last_y = wh / 2.0f; k->smooth_x = k->last_x; k->smooth_y = k->last_y;
+        k->rot_init = 1;
+    }
+    const float sf = 0.5f, sens = 0.2f;
+    if (rmb) {
+        if (k->first_mouse) {
+            k->last_x = mx; k->last_y = my; k->smooth_x = mx; k->smooth_y = my; k->first_mouse = 0;
+        } else {
+            k->rotates = 1;
+            k->smooth_x = k->smooth_x * (1 - sf) + mx * sf;
+            k->smooth_y = k->smooth_y * (1 - sf) + my * sf;
+            float xo = k->smooth_x - k->last_x, yo = k->smooth_y - k->last_y;
+            k->last_x = k->smooth_x; k->last_y = k->smooth_y;
+            xo *= -sens; yo *= -sens;
+            c->yaw += xo; c->pitch += yo;
+            c->pitch = fmaxf(-89.0f, fminf(89.0f, c->pitch));
+        }
+    } else {
+        k->first_mouse = 1; k->rotates = 0;
+    }
+    /* updatePosition (:131-157), movement speed 1 */
+    float vel = 1.0f * dt;
+    V3 prev = c->pos;
+    if (keys & 1u) c->pos = vsub(c->pos, muls(c->front, vel));
+    if (keys & 4u) c->pos = vadd(c->pos, muls(c->front, vel));
+    if (keys & 2u) c->pos = vsub(c->pos, muls(c->right, vel));
+    if (keys & 8u) c->pos = vadd(c->pos, muls(c->right, vel));
+    if (keys & 16u) c->pos = vadd(c->pos, muls(c->world_up, vel));
+    if (keys & 32u) c->pos = vsub(c->pos, muls(c->world_up, vel));
+    k->moves = !(c->pos.e[0] == prev.e[0] && c->pos.e[1] == prev.e[1] && c->pos.e[2] == prev.e[2]);
+    cam_update(c);
+    /* :52-71 */
+    if (keys & 64u) k->hq = !k->hq;
+    if (k->rotates || k->moves) { k->spp = 1; k->hq = 0; }
+    else if (k->hq) k->spp = 2000;
+    else k->spp = 1;
+    k->scale = 1.f / k->spp;
+}
+
+/* cam19 as oracle_camera; state8 = yaw, pitch, moving, rotating, high_quality, focus, spp, pixel_sample_scale */
+EXPORT void oracle_camctl_get(const void* p, float* cam19, float* state8) {
+    const CamCtl* k = (const CamCtl*)p;
+    const Cam* c = &k->c;
+    const V3* vs[6] = {&c->pos, &c->llc, &c->horiz, &c->vert, &c->right, &c->up};
+    for (int i = 0; i < 6; i++) memcpy(cam19 + 3 * i, vs[i]->e, 12);
+    cam19[18] = c->lens_r;
+    state8[0] = c->yaw; state8[1] = c->pitch; state8[2] = (float)k->moves; state8[3] = (float)k->rotates;
+    state8[4] = (float)k->hq; state8[5] = c->focus; state8[6] = (float)k->spp; state8[7] = k->scale;
 }

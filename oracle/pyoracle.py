@@ -41,6 +41,13 @@ def lib():
         L.oracle_rng_init.argtypes = [u64, u64, P]
         L.oracle_rng_draw.argtypes = [P, i32, P, P]
         L.oracle_seq_matrix.argtypes = [i32, P]
+        L.oracle_render_rng.argtypes = [P, P, i32, i32, i32, i32, i32, P, i32, P, P, P]
+        L.oracle_render_rng.restype = i32
+        L.oracle_camctl_new.argtypes = [C.c_float, C.c_float, P, P, C.c_float, C.c_float]
+        L.oracle_camctl_new.restype = P
+        L.oracle_camctl_free.argtypes = [P]
+        L.oracle_camctl_update.argtypes = [P, C.c_float, i32, i32, C.c_float, C.c_float, i32, C.c_uint, i32]
+        L.oracle_camctl_get.argtypes = [P, P, P]
         _lib = L
     return _lib
 
@@ -101,6 +108,48 @@ class OracleScene:
                             x0, y0, x1, y1, nthreads, _p(s), _p(rgba), _p(cnt))
         return s, rgba, {"rays": int(cnt[0]), "box_tests": int(cnt[1]), "tri_tests": int(cnt[2]),
                          "sphere_tests": int(cnt[3])}
+
+
+    def render_rng(self, cam19, w, h, spp, rng_state, max_bounces=20, nthreads=None, spp_total=None):
+        """One frame continuing the per-pixel RNG state (h*w*6 uint32, updated in place), like consecutive
+        CUDARenderer::render calls over one curandState array."""
+        assert rng_state.dtype == np.uint32 and rng_state.size == w * h * 6 and rng_state.flags.c_contiguous
+        s = np.zeros((h, w, 3), np.float32)
+        rgba = np.zeros((h, w, 4), np.uint8)
+        cnt = np.zeros(4, np.uint64)
+        cam = np.ascontiguousarray(cam19, np.float32)
+        lib().oracle_render_rng(self.h, _p(cam), w, h, spp, spp_total or spp, max_bounces, _p(rng_state),
+                                nthreads or os.cpu_count() or 1, _p(s), _p(rgba), _p(cnt))
+        return s, rgba, {"rays": int(cnt[0])}
+
+
+class CameraController:
+    """Camera::updateCamera restated (oracle_camctl_*): input per frame = mouse x/y, right button,
+    key bits (W=1 A=2 S=4 D=8 Space=16 LControl=32 F=64), focus steps."""
+
+    def __init__(self, aspect=16.0 / 9.0, vfov=80.0, pos=(0.0, 4.0, 4.0), up=(0.0, 1.0, 0.0), aperture=0.000001,
+                 focus=None):
+        pos = np.asarray(pos, np.float32)
+        if focus is None:
+            focus = float(np.sqrt(np.float32(np.dot(pos, pos))))
+        self.h = lib().oracle_camctl_new(C.c_float(aspect), C.c_float(vfov), _p(pos),
+                                         _p(np.asarray(up, np.float32)), C.c_float(aperture), C.c_float(focus))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_camctl_free(self.h)
+            self.h = None
+
+    def update(self, dt, ww, wh, mouse_x=0.0, mouse_y=0.0, right_mouse=False, keys=0, focus_steps=0):
+        lib().oracle_camctl_update(self.h, C.c_float(dt), ww, wh, C.c_float(mouse_x), C.c_float(mouse_y),
+                                   int(bool(right_mouse)), keys, focus_steps)
+
+    def get(self):
+        cam = np.zeros(19, np.float32)
+        st = np.zeros(8, np.float32)
+        lib().oracle_camctl_get(self.h, _p(cam), _p(st))
+        return cam, {"yaw": float(st[0]), "pitch": float(st[1]), "moving": bool(st[2]), "rotating": bool(st[3]),
+                     "high_quality": bool(st[4]), "focus": float(st[5]), "spp": int(st[6]), "scale": float(st[7])}
 
 
 def camera(aspect=16.0 / 9.0, vfov=80.0, pos=(0.0, 0.0, 0.3), up=(0.0, 1.0, 0.0), aperture=0.000001,

@@ -184,10 +184,19 @@ class Renderer:
         h = C.c_void_p()
         check(_lib.hip().crt_renderer_create(int(width), int(height), int(device), C.byref(h)), "crt_renderer_create")
         self.h, self.width, self.height, self.device = h, width, height, device
+        self._owned = True
+
+    @classmethod
+    def _borrow(cls, handle, width: int, height: int, device: int, owner):
+        """A view of a renderer owned by someone else (e.g. a Viewer); never destroys it."""
+        r = cls.__new__(cls)
+        r.h, r.width, r.height, r.device, r._owned, r._owner = C.c_void_p(handle), width, height, device, False, owner
+        return r
 
     def close(self):
         if getattr(self, "h", None):
-            _lib.hip().crt_renderer_destroy(self.h)
+            if getattr(self, "_owned", True):
+                _lib.hip().crt_renderer_destroy(self.h)
             self.h = None
 
     __del__ = close
@@ -315,6 +324,81 @@ def device_count() -> int:
     n = C.c_int(0)
     check(_lib.hip().crt_device_count(C.byref(n)), "device_count")
     return n.value
+
+
+KEY_W, KEY_A, KEY_S, KEY_D, KEY_SPACE, KEY_LCONTROL, KEY_F = 1, 2, 4, 8, 16, 32, 64
+
+
+def _input(mouse_x=0.0, mouse_y=0.0, right_mouse=False, keys=0, focus_steps=0) -> _lib.CrthInput:
+    return _lib.CrthInput(float(mouse_x), float(mouse_y), int(bool(right_mouse)), int(keys), int(focus_steps))
+
+
+class CameraController:
+    """CRT::Camera + Camera::updateCamera on the host (crth_camera_*; Camera.cuh:46-157). No GPU."""
+
+    def __init__(self, aspect=16.0 / 9.0, vfov=80.0, pos=(0.0, 4.0, 4.0), up=(0.0, 1.0, 0.0), aperture=0.000001,
+                 focus=None):
+        pos = np.asarray(pos, np.float32)
+        if focus is None:
+            focus = float(np.sqrt(np.float32(np.dot(pos, pos))))
+        h = C.c_void_p()
+        check_host(_lib.host().crth_camera_create(aspect, vfov, _p(pos), _p(np.asarray(up, np.float32)), aperture,
+                                                  focus, C.byref(h)), "crth_camera_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.host().crth_camera_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def update(self, dt, ww, wh, **inp):
+        check_host(_lib.host().crth_camera_update(self.h, dt, ww, wh, C.byref(_input(**inp))), "crth_camera_update")
+
+    def get(self):
+        d = CameraDesc()
+        st = np.zeros(6, np.float32)
+        check_host(_lib.host().crth_camera_get(self.h, C.byref(d), _p(st)), "crth_camera_get")
+        return d, {"yaw": float(st[0]), "pitch": float(st[1]), "moving": bool(st[2]), "rotating": bool(st[3]),
+                   "high_quality": bool(st[4]), "focus": float(st[5])}
+
+
+class Viewer:
+    """The reference's Raytracer loop, headless (crth_viewer_*; Raytracer.h:52-102): one frame() per
+    updateAndRender with the input the window would have delivered."""
+
+    def __init__(self, obj_files, width, height, device=0, bvh="reference", aspect=16.0 / 9.0, vfov=80.0,
+                 aperture=0.000001, pos=None, focus=0.0, seed=41, accumulate=False, **scene_kw):
+        files = [str(f).encode() for f in obj_files]
+        arr = (C.c_char_p * len(files))(*files)
+        opts = scene_options(bvh, **scene_kw)
+        pos_a = None if pos is None else np.asarray(pos, np.float32)
+        h = C.c_void_p()
+        check_host(_lib.host().crth_viewer_create(arr, len(files), device, C.byref(opts), width, height, aspect, vfov,
+                                                  aperture, None if pos_a is None else _p(pos_a), focus, seed,
+                                                  int(bool(accumulate)), C.byref(h)), "crth_viewer_create")
+        self.h, self.width, self.height, self.device = h, width, height, device
+        self.renderer = Renderer._borrow(_lib.host().crth_viewer_renderer(h), width, height, device, self)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.renderer.h = None
+            _lib.host().crth_viewer_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def frame(self, dt=1.0 / 60.0, **inp) -> dict:
+        fi = _lib.CrthFrameInfo()
+        check_host(_lib.host().crth_viewer_frame(self.h, dt, C.byref(_input(**inp)), C.byref(fi)), "crth_viewer_frame")
+        return {"frame": fi.frame, "spp": fi.spp, "accumulated": fi.accumulated, "moving": bool(fi.moving),
+                "high_quality": bool(fi.high_quality), "kernel_ms": fi.kernel_ms, "frame_ms": fi.frame_ms}
+
+    def camera(self) -> CameraDesc:
+        d = CameraDesc()
+        check_host(_lib.host().crth_viewer_camera(self.h, C.byref(d)), "crth_viewer_camera")
+        return d
 
 
 IMAGE_FORMATS = {"ppm": 0, "png": 1}

@@ -34,6 +34,16 @@ class CameraDesc(C.Structure):
                 ("lens_radius", C.c_float), ("samples_per_pixel", C.c_int32), ("pixel_sample_scale", C.c_float)]
 
 
+class CrthInput(C.Structure):        # crt_host.h crth_input
+    _fields_ = [("mouse_x", C.c_float), ("mouse_y", C.c_float), ("right_mouse", C.c_int32), ("keys", C.c_uint32),
+                ("focus_steps", C.c_int32)]
+
+
+class CrthFrameInfo(C.Structure):    # crt_host.h crth_frame_info
+    _fields_ = [("frame", C.c_int64), ("spp", C.c_int32), ("accumulated", C.c_int32), ("moving", C.c_int32),
+                ("high_quality", C.c_int32), ("kernel_ms", C.c_float), ("frame_ms", C.c_double)]
+
+
 class SceneDesc(C.Structure):
     _fields_ = [("positions", C.c_void_p), ("n_positions", C.c_uint64), ("indices", C.c_void_p),
                 ("n_indices", C.c_uint64), ("face_materials", C.c_void_p), ("n_faces", C.c_uint64),
@@ -91,6 +101,8 @@ HIP_SYMBOLS = [
 HOST_SYMBOLS = [
     "crth_scene_load", "crth_scene_destroy", "crth_scene_desc", "crth_scene_upload", "crth_scene_upload_ex", "crth_scene_counts",
     "crth_scene_loader_arrays", "crth_camera", "crth_last_error", "crth_encode_image", "crth_write_image",
+    "crth_camera_create", "crth_camera_update", "crth_camera_get", "crth_camera_destroy",
+    "crth_viewer_create", "crth_viewer_frame", "crth_viewer_camera", "crth_viewer_renderer", "crth_viewer_destroy",
 ]
 
 _hip = None
@@ -177,6 +189,12 @@ def host():
             "crth_last_error": ([], C.c_char_p),
             "crth_encode_image": ([i32, P, i32, i32, i32, P, P], i32),
             "crth_write_image": ([C.c_char_p, P, i32, i32, i32], i32),
+            "crth_camera_create": ([f32, f32, P, P, f32, f32, P], i32),
+            "crth_camera_update": ([P, f32, i32, i32, P], i32),
+            "crth_camera_get": ([P, P, P], i32), "crth_camera_destroy": ([P], None),
+            "crth_viewer_create": ([P, i32, i32, P, i32, i32, f32, f32, f32, P, f32, C.c_ulonglong, i32, P], i32),
+            "crth_viewer_frame": ([P, f32, P, P], i32), "crth_viewer_camera": ([P, P], i32),
+            "crth_viewer_renderer": ([P], P), "crth_viewer_destroy": ([P], None),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)

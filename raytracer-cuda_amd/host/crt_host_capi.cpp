@@ -1,10 +1,12 @@
 // crt_host_capi.cpp — C ABI over the host C++ scene pipeline (include/crt_host.h).
 #include <cstring>
+#include <memory>
 #include <exception>
 #include <string>
 
 #include "crt/Camera.h"
 #include "crt/ImageIO.h"
+#include "crt/Raytracer.h"
 #include "crt/SceneManager.h"
 #include "crt_host.h"
 
@@ -15,7 +17,32 @@ struct crth_scene {
     std::vector<int32_t> fmat0;
 };
 
+struct crth_camera_ctl {
+    CRT::Camera cam;
+};
+
+struct crth_viewer {
+    std::unique_ptr<CRT::Raytracer> rt;
+};
+
 static thread_local std::string g_err;
+
+static CRT::InputState to_input(const crth_input* in) {
+    CRT::InputState s;
+    if (!in) return s;
+    s.mouseX = in->mouse_x;
+    s.mouseY = in->mouse_y;
+    s.rightMouse = in->right_mouse != 0;
+    s.keyW = (in->keys & CRTH_KEY_W) != 0;
+    s.keyA = (in->keys & CRTH_KEY_A) != 0;
+    s.keyS = (in->keys & CRTH_KEY_S) != 0;
+    s.keyD = (in->keys & CRTH_KEY_D) != 0;
+    s.keySpace = (in->keys & CRTH_KEY_SPACE) != 0;
+    s.keyLControl = (in->keys & CRTH_KEY_LCONTROL) != 0;
+    s.keyF = (in->keys & CRTH_KEY_F) != 0;
+    s.focusSteps = in->focus_steps;
+    return s;
+}
 
 extern "C" {
 
@@ -114,6 +141,96 @@ int crth_camera(float aspect, float vfov, const float* pos3, const float* up3, f
     *out = cam.toDesc();
     return CRT_OK;
 }
+
+int crth_camera_create(float aspect, float vfov, const float* pos3, const float* up3, float aperture, float focus,
+                       crth_camera_ctl** out) {
+    if (!pos3 || !up3 || !out) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    *out = new crth_camera_ctl{CRT::Camera(aspect, vfov, CRT::Vec3(pos3[0], pos3[1], pos3[2]), CRT::Vec3(0, 0, 0),
+                                       CRT::Vec3(up3[0], up3[1], up3[2]), aperture, focus)};
+    return CRT_OK;
+}
+
+int crth_camera_update(crth_camera_ctl* c, float dt, int w, int h, const crth_input* in) {
+    if (!c || !in) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    const CRT::InputState s = to_input(in);
+    for (int k = 0; k < s.focusSteps; ++k) c->cam.adjustFocusDistance(0.1f);   // WindowManager.h:64-67
+    for (int k = 0; k > s.focusSteps; --k) c->cam.adjustFocusDistance(-0.1f);
+    c->cam.updateCamera(dt, w, h, s);
+    return CRT_OK;
+}
+
+int crth_camera_get(const crth_camera_ctl* c, crt_camera_desc* desc, float* st) {
+    if (!c) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    if (desc) *desc = c->cam.toDesc();
+    if (st) {
+        st[0] = c->cam.yaw();
+        st[1] = c->cam.pitch();
+        st[2] = c->cam.isMoving() ? 1.f : 0.f;
+        st[3] = c->cam.isRotating() ? 1.f : 0.f;
+        st[4] = c->cam.isHighQuality() ? 1.f : 0.f;
+        st[5] = c->cam.getFocusDistance();
+    }
+    return CRT_OK;
+}
+
+void crth_camera_destroy(crth_camera_ctl* c) { delete c; }
+
+int crth_viewer_create(const char* const* files, int n_files, int device, const crt_scene_options* opts, int width,
+                       int height, float aspect, float vfov, float aperture, const float* pos3, float focus,
+                       unsigned long long seed, int accumulate, crth_viewer** out) {
+    if (!out || (n_files > 0 && !files) || n_files < 0 || width <= 0 || height <= 0) {
+        g_err = "bad argument";
+        return CRT_ERR_INVALID_ARGUMENT;
+    }
+    *out = nullptr;
+    try {
+        CRT::RaytracerOptions o;
+        for (int i = 0; i < n_files; ++i) o.modelFiles.emplace_back(files[i]);
+        if (opts) o.scene = *opts;
+        o.seed = seed;
+        o.device = device;
+        if (pos3) { o.hasPose = true; o.position = CRT::Vec3(pos3[0], pos3[1], pos3[2]); }
+        o.focusDist = focus;
+        o.accumulate = accumulate != 0;
+        auto v = std::make_unique<crth_viewer>();
+        v->rt = std::make_unique<CRT::Raytracer>(width, height, aspect, vfov, aperture, o);
+        *out = v.release();
+        return CRT_OK;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return CRT_ERR_INVALID_ARGUMENT;
+    }
+}
+
+int crth_viewer_frame(crth_viewer* v, float dt, const crth_input* in, crth_frame_info* info) {
+    if (!v || !in) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    try {
+        const CRT::FrameInfo fi = v->rt->updateAndRender(dt, to_input(in));
+        if (info) {
+            info->frame = fi.frame;
+            info->spp = fi.spp;
+            info->accumulated = fi.accumulated;
+            info->moving = fi.moving;
+            info->high_quality = fi.highQuality;
+            info->kernel_ms = fi.kernelMs;
+            info->frame_ms = fi.frameMs;
+        }
+        return CRT_OK;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return CRT_ERR_HIP;
+    }
+}
+
+int crth_viewer_camera(const crth_viewer* v, crt_camera_desc* out) {
+    if (!v || !out) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
+    *out = v->rt->camera().toDesc();
+    return CRT_OK;
+}
+
+crt_renderer* crth_viewer_renderer(crth_viewer* v) { return v ? v->rt->renderer().handle() : nullptr; }
+
+void crth_viewer_destroy(crth_viewer* v) { delete v; }
 
 int crth_encode_image(int format, const uint8_t* rgba, int w, int h, int flip, uint8_t* out, uint64_t* size) {
     if (!rgba || !size || w <= 0 || h <= 0 || (format != CRTH_IMAGE_PPM && format != CRTH_IMAGE_PNG)) {

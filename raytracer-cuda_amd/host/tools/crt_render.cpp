@@ -1,6 +1,6 @@
 // crt_render — headless equivalent of the reference's EntryPoint.cu:14-42 + Raytracer.h:77-102:
 // build the scene with SceneManager, set the camera, render one frame with CUDARenderer and
-// write it as a binary PPM (rows flipped like WindowManager::drawFrame's flipVertically).
+// write it as PNG or binary PPM by extension (rows flipped like WindowManager::drawFrame's flipVertically).
 //
 //   crt_render [-w W] [-h H] [-spp N] [-seed S] [-o out.ppm] [-pos x y z] [-fov deg] [-bvh reference|rebuilt]
 //              [-leaf N] model.obj...
@@ -13,6 +13,7 @@
 
 #include "crt/CUDARenderer.h"
 #include "crt/Camera.h"
+#include "crt/ImageIO.h"
 #include "crt/SceneManager.h"
 
 int main(int argc, char** argv) {
@@ -22,7 +23,7 @@ int main(int argc, char** argv) {
         unsigned long long seed = 41;
         float fov = 80.0f, aperture = 0.000001f;
         float pos[3] = {0.f, 0.f, 0.3f};
-        std::string out = "frame.ppm";
+        std::string out = "frame.png";
         std::vector<std::string> files;
         crt_scene_options opts{};
         for (int i = 1; i < argc; ++i) {
@@ -61,12 +62,7 @@ int main(int argc, char** argv) {
         crt_work_counters c{};
         CRT_CHECK(crt_renderer_get_counters(renderer.handle(), &c));
         std::vector<uint8_t> img = renderer.readImage();
-        FILE* f = std::fopen(out.c_str(), "wb");
-        if (!f) throw std::runtime_error("cannot open " + out);
-        std::fprintf(f, "P6\n%d %d\n255\n", W, H);
-        for (int y = H - 1; y >= 0; --y)                       // flipVertically (WindowManager.h:88)
-            for (int x = 0; x < W; ++x) std::fwrite(&img[4 * ((size_t)y * W + x)], 1, 3, f);
-        std::fclose(f);
+        CRT::writeImage(out, img.data(), W, H, true);   // flipVertically (WindowManager.h:88); .png or .ppm
         double setup = std::chrono::duration<double>(t1 - t0).count();
         double frame = std::chrono::duration<double>(t2 - t1).count();
         std::printf("{\"width\": %d, \"height\": %d, \"spp\": %d, \"rays\": %llu, \"setup_s\": %.4f, \"frame_s\": %.4f, "

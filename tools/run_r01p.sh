@@ -1,0 +1,15 @@
+# interactive loop: GPU tests incl. the viewer, then frame-time runs of the headless loop
+set -e
+OUT=gpurun_out/r01p
+mkdir -p $OUT
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_viewer.py -x -v --timeout 240 --timeout-method thread > $OUT/pytest_viewer.log 2>&1
+FILES=$(python3 -c "import sys; sys.path.insert(0,'raytracer-cuda_amd'); from crt_amd import assets; print(' '.join(assets.scene_files('cornell_bunny')))")
+V=raytracer-cuda_amd/bin/crt_viewer
+timeout -k 10 120 $V -frames 600 -script still -bvh rebuilt $FILES > $OUT/viewer_still_rebuilt.json
+timeout -k 10 120 $V -frames 600 -script still -bvh reference $FILES > $OUT/viewer_still_reference.json
+timeout -k 10 120 $V -frames 600 -script orbit -bvh rebuilt $FILES > $OUT/viewer_orbit_rebuilt.json
+timeout -k 10 120 $V -frames 600 -script walk -bvh rebuilt $FILES > $OUT/viewer_walk_rebuilt.json
+timeout -k 10 120 $V -frames 600 -script still -bvh rebuilt -accumulate -o $OUT/accumulated_600spp.png $FILES > $OUT/viewer_accumulate_rebuilt.json
+timeout -k 10 120 $V -frames 3 -script hq -bvh rebuilt -o $OUT/hq_2000spp.png $FILES > $OUT/viewer_hq_rebuilt.json
+timeout -k 10 120 $V -w 1280 -frames 600 -script still -bvh rebuilt $FILES > $OUT/viewer_still_rebuilt_720p.json
+echo done
