@@ -266,6 +266,20 @@ float crt_renderer_last_kernel_ms(crt_renderer* r);
  * "crt_render_kernel<false, 4, 6>" (empty before the first launch and for variant 5). */
 const char* crt_renderer_last_kernel_name(const crt_renderer* r);
 
+/* ---- GPU-parallel mesh BVH build (replaces Mesh::buildBVHMesh <<<1,1>>>, Mesh.cuh:121-264, and the Mesh ctor
+ * box, Mesh.cuh:39-47; launched by initMesh, CUDAKernels.h:28-33) ----
+ * Same node array (reference allocation order, crt_bvh_node_desc as the host builder emits it) and the same
+ * in-place permutation of indices / face_materials (swap_triplet, Core.cuh:25-39) as the reference's single-thread
+ * builder, computed level-parallel on `device` (see csrc/crt_bvh_build.hip).  positions: vertex_count slots (xyz);
+ * indices: index_count local indices (multiple of 3), permuted in place; nodes: capacity 2*(index_count/3) - 1;
+ * mesh_box: min xyz, max xyz.  build_ms (optional): device time from the first upload to the last kernel.
+ * Returns CRT_ERR_UNSUPPORTED (nothing written) for meshes where the reference's node cap decides the tree (a split
+ * with an empty side) or index_count % 3 != 0: the caller uses the sequential host builder then.  Box bounds may
+ * differ from a sequential build in the sign of a zero only. */
+int crt_build_mesh_bvh(int device, const float* positions, uint32_t vertex_count, uint32_t* indices,
+                       int32_t* face_materials, uint32_t index_count, crt_bvh_node_desc* nodes, int32_t* node_count,
+                       float mesh_box[6], float* build_ms);
+
 /* ---- self-test of the arithmetic the kernel depends on (IEEE f32/f64 div/sqrt) ---- */
 /* For n inputs a[i], b[i] (f32) computes on the device: a/b, sqrtf(|a|), 1/a, (double)sqrt((double)|a|)
  * into out[4*i..4*i+3] (the last one converted to float bits as a double->float cast). */

@@ -21,6 +21,11 @@ typedef struct crth_scene crth_scene;
 
 /* Load + build on the host (SceneManager::initializeScene minus the upload). */
 int crth_scene_load(const char* const* obj_files, int n_files, crth_scene** out);
+/* crth_scene_load with the mesh BVHs built on GPU `build_device` (crt_build_mesh_bvh: the same trees as the host
+ * restatement; meshes the reference's node cap decides fall back to the host); build_device < 0 = host. */
+int crth_scene_load_ex(const char* const* obj_files, int n_files, int build_device, crth_scene** out);
+/* Device milliseconds of the GPU mesh BVH builds of the last load (0 for host builds). */
+double crth_scene_build_ms(const crth_scene* s);
 void crth_scene_destroy(crth_scene* s);
 /* The flat description handed to crt_scene_create (pointers stay owned by `s`). */
 int crth_scene_desc(const crth_scene* s, crt_scene_desc* out);
@@ -41,6 +46,11 @@ int crth_scene_loader_arrays(const crth_scene* s, float* positions, uint32_t* in
 /* CRT::Camera(aspect, fov, pos, target(ignored), up, aperture, focus) + setYawPitch + spp. */
 int crth_camera(float aspect, float vfov, const float* pos3, const float* up3, float aperture, float focus,
                 float yaw, float pitch, int spp, crt_camera_desc* out);
+
+/* The host restatement of Mesh::buildBVHMesh + the Mesh ctor box (Mesh.cuh:39-47, :121-264), same contract as
+ * crt_build_mesh_bvh (crt_hip.h) but sequential on the host, exactly the reference's loop.  No GPU needed. */
+int crth_build_mesh_bvh(const float* positions, uint32_t vertex_count, uint32_t* indices, int32_t* face_materials,
+                        uint32_t index_count, crt_bvh_node_desc* nodes, int32_t* node_count, float mesh_box[6]);
 
 /* ---- interactive loop (Raytracer.h:52-102, Camera.cuh:46-157), headless ----
  * The reference polls SFML each frame; here the caller passes what it would have polled. */

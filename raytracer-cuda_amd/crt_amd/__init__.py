@@ -49,13 +49,20 @@ def camera_floats(d: CameraDesc) -> np.ndarray:
 class HostScene:
     """SceneManager host half: load OBJ files, normalise, build mesh + scene BVHs (C++)."""
 
-    def __init__(self, obj_files):
+    def __init__(self, obj_files, build_device=None):
+        """build_device: None = mesh BVHs built by the host restatement; k = on GPU k (crt_build_mesh_bvh,
+        same trees)."""
         files = [str(f) for f in obj_files]
         arr = (C.c_char_p * len(files))(*[f.encode() for f in files])
         h = C.c_void_p()
-        check_host(_lib.host().crth_scene_load(arr, len(files), C.byref(h)), "crth_scene_load")
+        bd = -1 if build_device is None else int(build_device)
+        check_host(_lib.host().crth_scene_load_ex(arr, len(files), bd, C.byref(h)), "crth_scene_load_ex")
         self.h = h
         self.files = files
+
+    def device_build_ms(self) -> float:
+        """Device time of the GPU mesh BVH builds of this load (0.0 for host builds)."""
+        return float(_lib.host().crth_scene_build_ms(self.h))
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -369,10 +376,10 @@ class Viewer:
     updateAndRender with the input the window would have delivered."""
 
     def __init__(self, obj_files, width, height, device=0, bvh="reference", aspect=16.0 / 9.0, vfov=80.0,
-                 aperture=0.000001, pos=None, focus=0.0, seed=41, accumulate=False, **scene_kw):
+                 aperture=0.000001, pos=None, focus=0.0, seed=41, accumulate=False, bvh_width=0, **scene_kw):
         files = [str(f).encode() for f in obj_files]
         arr = (C.c_char_p * len(files))(*files)
-        opts = scene_options(bvh, **scene_kw)
+        opts = scene_options(bvh, width=bvh_width, **scene_kw)
         pos_a = None if pos is None else np.asarray(pos, np.float32)
         h = C.c_void_p()
         check_host(_lib.host().crth_viewer_create(arr, len(files), device, C.byref(opts), width, height, aspect, vfov,
@@ -426,3 +433,39 @@ def write_image(path: str, rgba: np.ndarray, flip: bool = True) -> None:
         raise CrtError("rgba must be (H, W, 4) uint8")
     check_host(_lib.host().crth_write_image(str(path).encode(), _p(a), a.shape[1], a.shape[0], int(flip)),
                "crth_write_image")
+
+
+NODE_DTYPE = np.dtype([("bmin", "<f4", 3), ("bmax", "<f4", 3), ("left", "<i4"), ("right", "<i4"),
+                       ("obj_index", "<i4"), ("obj_count", "<i4"), ("is_leaf", "<i4")])   # crt_bvh_node_desc
+
+
+def build_mesh_bvh(positions, indices, face_materials, device=None):
+    """Mesh::buildBVHMesh + Mesh ctor box (Mesh.cuh:39-47, :121-264) on one mesh.
+
+    device=None: the sequential host restatement (crth_build_mesh_bvh); device=k: the GPU-parallel build
+    on device k (crt_build_mesh_bvh).  Returns (nodes [NODE_DTYPE], permuted indices, permuted face
+    materials, mesh box (6,), device ms or None).  Raises CrtError; a GPU build that must defer to the
+    host builder raises with status CRT_ERR_UNSUPPORTED (-5)."""
+    pos = np.ascontiguousarray(positions, np.float32).reshape(-1)
+    idx = np.ascontiguousarray(indices, np.uint32).copy()
+    fm = np.ascontiguousarray(face_materials, np.int32).copy()
+    n_tri = len(idx) // 3
+    nodes = np.zeros(max(1, 2 * n_tri - 1), NODE_DTYPE)
+    cnt = C.c_int32(0)
+    box = np.zeros(6, np.float32)
+    if device is None:
+        rc = _lib.host().crth_build_mesh_bvh(_p(pos), len(pos) // 3, _p(idx), _p(fm), len(idx), _p(nodes),
+                                             C.byref(cnt), _p(box))
+        check_host(rc, "crth_build_mesh_bvh")
+        ms = None
+    else:
+        t = C.c_float(0)
+        rc = _lib.hip().crt_build_mesh_bvh(int(device), _p(pos), len(pos) // 3, _p(idx), _p(fm), len(idx), _p(nodes),
+                                           C.byref(cnt), _p(box), C.byref(t))
+        if rc != 0:
+            err = CrtError(f"crt_build_mesh_bvh failed (status {rc}): "
+                           f"{_lib.hip().crt_last_error().decode(errors='replace')}")
+            err.status = rc
+            raise err
+        ms = t.value
+    return nodes[:cnt.value], idx, fm, box, ms

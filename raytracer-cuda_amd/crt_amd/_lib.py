@@ -96,12 +96,13 @@ HIP_SYMBOLS = [
     "crt_renderer_last_kernel_name",
     "crt_renderer_attach_linear", "crt_renderer_set_kernel_variant", "crt_renderer_get_schedule_stats",
     "crt_renderer_set_regen_threshold", "crt_renderer_set_occupancy_target",
+    "crt_build_mesh_bvh",
     "crt_selftest_math", "crt_selftest_rng", "crt_selftest_scan", "crt_selftest_rcp",
 ]
 HOST_SYMBOLS = [
-    "crth_scene_load", "crth_scene_destroy", "crth_scene_desc", "crth_scene_upload", "crth_scene_upload_ex", "crth_scene_counts",
+    "crth_scene_load", "crth_scene_load_ex", "crth_scene_build_ms", "crth_scene_destroy", "crth_scene_desc", "crth_scene_upload", "crth_scene_upload_ex", "crth_scene_counts",
     "crth_scene_loader_arrays", "crth_camera", "crth_last_error", "crth_encode_image", "crth_write_image",
-    "crth_camera_create", "crth_camera_update", "crth_camera_get", "crth_camera_destroy",
+    "crth_build_mesh_bvh", "crth_camera_create", "crth_camera_update", "crth_camera_get", "crth_camera_destroy",
     "crth_viewer_create", "crth_viewer_frame", "crth_viewer_camera", "crth_viewer_renderer", "crth_viewer_destroy",
 ]
 
@@ -159,6 +160,7 @@ def hip():
             "crt_renderer_get_schedule_stats": ([P, P], i32),
             "crt_renderer_set_regen_threshold": ([P, i32], i32),
             "crt_renderer_set_occupancy_target": ([P, i32], i32),
+            "crt_build_mesh_bvh": ([i32, P, C.c_uint32, P, P, C.c_uint32, P, P, P, P], i32),
             "crt_selftest_math": ([P, P, i32, P, P], i32),
             "crt_selftest_rng": ([u64, P, i32, i32, P, P], i32),
             "crt_selftest_scan": ([P, i32, P], i32),
@@ -181,7 +183,8 @@ def host():
         L = C.CDLL(str(HOST_LIB))
         P, i32, f32 = C.c_void_p, C.c_int, C.c_float
         sig = {
-            "crth_scene_load": ([P, i32, P], i32), "crth_scene_destroy": ([P], None),
+            "crth_scene_load": ([P, i32, P], i32), "crth_scene_load_ex": ([P, i32, i32, P], i32),
+            "crth_scene_build_ms": ([P], C.c_double), "crth_scene_destroy": ([P], None),
             "crth_scene_desc": ([P, P], i32), "crth_scene_upload": ([P, i32, P], i32),
             "crth_scene_upload_ex": ([P, i32, P, P], i32),
             "crth_scene_counts": ([P, P], i32), "crth_scene_loader_arrays": ([P, P, P, P, P, P], i32),
@@ -190,6 +193,7 @@ def host():
             "crth_encode_image": ([i32, P, i32, i32, i32, P, P], i32),
             "crth_write_image": ([C.c_char_p, P, i32, i32, i32], i32),
             "crth_camera_create": ([f32, f32, P, P, f32, f32, P], i32),
+            "crth_build_mesh_bvh": ([P, C.c_uint32, P, P, C.c_uint32, P, P, P], i32),
             "crth_camera_update": ([P, f32, i32, i32, P], i32),
             "crth_camera_get": ([P, P, P], i32), "crth_camera_destroy": ([P], None),
             "crth_viewer_create": ([P, i32, i32, P, i32, i32, f32, f32, f32, P, f32, C.c_ulonglong, i32, P], i32),

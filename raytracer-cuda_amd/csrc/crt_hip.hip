@@ -30,6 +30,7 @@ static int set_error(int code, const std::string& msg) {
     g_last_error = msg;
     return code;
 }
+int crtx_set_error(int code, const std::string& msg) { return set_error(code, msg); }   // crt_bvh_build.hip
 #define HIP_TRY(expr)                                                                           \
     do {                                                                                        \
         hipError_t e_ = (expr);                                                                 \

@@ -35,6 +35,7 @@ struct RaytracerOptions {
     Vec3 position{0.f, 4.f, 4.f};
     float focusDist = 0.f;                  // <= 0: |position - (0,0,0)|, the reference's rule
     bool accumulate = false;
+    int meshBuildDevice = -1;              // >= 0: mesh BVHs built on that GPU (same trees, SceneManager)
 };
 
 struct FrameInfo {
@@ -117,6 +118,7 @@ private:
         m_Renderer.initialize(config, m_Options.seed);
         if (!m_Options.modelFiles.empty()) m_SceneManager.setModelFiles(m_Options.modelFiles);
         m_SceneManager.setSceneOptions(m_Options.scene);
+        m_SceneManager.setMeshBuildDevice(m_Options.meshBuildDevice);
         m_SceneManager.initializeScene(config, m_Renderer.getRandState());
     }
 

@@ -23,6 +23,7 @@ void SceneManager::initializeScene(const CUDAHelpers::RenderConfig& renderConfig
 }
 
 void SceneManager::buildHostScene() {
+    m_DeviceBuildMs = 0.0;
     m_MeshData.clear();
     m_SceneMaterialsData.clear();
     initMeshes();
@@ -36,6 +37,27 @@ void SceneManager::uploadScene() {
     }
     crt_scene_desc d = sceneDesc();
     CRT_CHECK(crt_scene_create_ex(&d, m_Device, &m_SceneOptions, &m_Scene));
+}
+
+// GPU-parallel build of mesh i (crt_build_mesh_bvh: the same tree as buildMeshBVH).  false = the mesh needs the
+// sequential builder (the reference's node cap decides its tree); other failures throw.
+bool SceneManager::buildMeshOnDevice(int i, const float* pos, uint32_t* idx, int32_t* fm) {
+    const uint32_t nTri = m_IndexCounts[i] / 3;
+    std::vector<crt_bvh_node_desc> nodes(nTri > 0 ? 2 * (size_t)nTri - 1 : 0);
+    int32_t count = 0;
+    float box[6];
+    float ms = 0.f;
+    const int rc = crt_build_mesh_bvh(m_BuildDevice, pos, m_VertexCounts[i], idx, fm, m_IndexCounts[i], nodes.data(),
+                                      &count, box, &ms);
+    if (rc == CRT_ERR_UNSUPPORTED) return false;
+    CRT_CHECK(rc);
+    nodes.resize((size_t)count);
+    m_MeshBVH[i].swap(nodes);
+    m_MeshBoxes[i].x = CRT::Interval(box[0], box[3]);
+    m_MeshBoxes[i].y = CRT::Interval(box[1], box[4]);
+    m_MeshBoxes[i].z = CRT::Interval(box[2], box[5]);
+    m_DeviceBuildMs += ms;
+    return true;
 }
 
 // :100-196
@@ -73,9 +95,12 @@ void SceneManager::initMeshes() {
             if (m_Indices[m_IndexOffsets[i] + k] >= m_VertexCounts[i])
                 throw std::runtime_error("mesh index out of range of its vertex slots");
         // Mesh ctor + buildBVHMesh (CUDAKernels.h:92-100, Mesh.cuh:18-53)
-        CRT::BuildStatus st = CRT::buildMeshBVH(m_Positions.data() + 3 * (size_t)m_VertexOffsets[i], m_VertexCounts[i],
-                                                m_Indices.data() + m_IndexOffsets[i], m_FaceMats.data() + m_FaceMatOffsets[i],
-                                                m_IndexCounts[i], &m_MeshBoxes[i], &m_MeshBVH[i]);
+        const float* pos = m_Positions.data() + 3 * (size_t)m_VertexOffsets[i];
+        uint32_t* idx = m_Indices.data() + m_IndexOffsets[i];
+        int32_t* fm = m_FaceMats.data() + m_FaceMatOffsets[i];
+        if (m_BuildDevice >= 0 && buildMeshOnDevice(i, pos, idx, fm)) continue;
+        CRT::BuildStatus st = CRT::buildMeshBVH(pos, m_VertexCounts[i], idx, fm, m_IndexCounts[i], &m_MeshBoxes[i],
+                                                &m_MeshBVH[i]);
         if (!st.ok) throw std::runtime_error(st.error);
     }
     for (int i = 0; i < n; i++) {

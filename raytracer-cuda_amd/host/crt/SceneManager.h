@@ -44,6 +44,10 @@ public:
     // Acceleration structure of the device scene (default CRT_BVH_REFERENCE, bit-exact); applies at uploadScene.
     void setSceneOptions(const crt_scene_options& opts) { m_SceneOptions = opts; }
     const std::vector<std::string>& modelFiles() const { return m_ModelFiles; }
+    // Where the mesh BVHs are built: -1 = the host restatement (default), k >= 0 = GPU k (crt_build_mesh_bvh, the
+    // same trees; meshes whose tree the reference's node cap decides still build on the host).
+    void setMeshBuildDevice(int device) { m_BuildDevice = device; }
+    double deviceBuildMs() const { return m_DeviceBuildMs; }   // device time of the GPU mesh builds
 
     // SceneManager::initializeScene (SceneManager.h:77-98).  randState is accepted for API
     // compatibility and unused (the reference passes it through and never draws from it).
@@ -73,6 +77,7 @@ private:
     void initMeshes();
     void loadObject(const std::string& filename, std::vector<MeshData>& meshDataList);
     void createWorld();
+    bool buildMeshOnDevice(int i, const float* pos, uint32_t* idx, int32_t* fm);
 
     int m_Width, m_Height, m_Device;
     std::vector<std::string> m_ModelFiles{"assets/models/CornellBox-Original.obj", "assets/models/bunny.obj"};
@@ -93,4 +98,6 @@ private:
     std::vector<crt_bvh_node_desc> m_SceneBVH;
     crt_scene* m_Scene = nullptr;
     crt_scene_options m_SceneOptions{};
+    int m_BuildDevice = -1;
+    double m_DeviceBuildMs = 0.0;
 };

@@ -48,7 +48,11 @@ extern "C" {
 
 const char* crth_last_error(void) { return g_err.c_str(); }
 
-int crth_scene_load(const char* const* files, int n, crth_scene** out) {
+int crth_scene_load(const char* const* files, int n, crth_scene** out) { return crth_scene_load_ex(files, n, -1, out); }
+
+double crth_scene_build_ms(const crth_scene* s) { return s ? s->sm.deviceBuildMs() : 0.0; }
+
+int crth_scene_load_ex(const char* const* files, int n, int build_device, crth_scene** out) {
     if (!files || n < 0 || !out) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
     *out = nullptr;
     try {
@@ -56,6 +60,7 @@ int crth_scene_load(const char* const* files, int n, crth_scene** out) {
         std::vector<std::string> v;
         for (int i = 0; i < n; ++i) v.emplace_back(files[i]);
         s->sm.setModelFiles(v);
+        s->sm.setMeshBuildDevice(build_device);
         s->sm.buildHostScene();
         // rebuild the unpermuted arrays from MeshData (the loader output)
         for (const auto& md : s->sm.meshData()) {
@@ -139,6 +144,27 @@ int crth_camera(float aspect, float vfov, const float* pos3, const float* up3, f
     if (yaw != -90.0f || pitch != 0.0f) cam.setYawPitch(yaw, pitch);
     cam.setSamplesPerPixel(spp);
     *out = cam.toDesc();
+    return CRT_OK;
+}
+
+int crth_build_mesh_bvh(const float* positions, uint32_t vertex_count, uint32_t* indices, int32_t* face_materials,
+                        uint32_t index_count, crt_bvh_node_desc* nodes, int32_t* node_count, float mesh_box[6]) {
+    if (!node_count || !mesh_box || (vertex_count && !positions) || (index_count && (!indices || !face_materials))) {
+        g_err = "bad argument";
+        return CRT_ERR_INVALID_ARGUMENT;
+    }
+    std::vector<crt_bvh_node_desc> out;
+    CRT::AABB box;
+    const CRT::BuildStatus st =
+        CRT::buildMeshBVH(positions, vertex_count, indices, face_materials, index_count, &box, &out);
+    if (!st.ok) { g_err = st.error; return CRT_ERR_INVALID_ARGUMENT; }
+    if (!out.empty()) {
+        if (!nodes) { g_err = "null nodes"; return CRT_ERR_INVALID_ARGUMENT; }
+        std::memcpy(nodes, out.data(), out.size() * sizeof(crt_bvh_node_desc));
+    }
+    *node_count = (int32_t)out.size();
+    mesh_box[0] = box.x.min; mesh_box[1] = box.y.min; mesh_box[2] = box.z.min;
+    mesh_box[3] = box.x.max; mesh_box[4] = box.y.max; mesh_box[5] = box.z.max;
     return CRT_OK;
 }
 
