@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--leaf-size", type=int, default=4)
     ap.add_argument("--traversal-cost", type=float, default=2.0)
     ap.add_argument("--no-parity", action="store_true", help="skip the reference-BVH parity frame")
+    ap.add_argument("--host-build", action="store_true",
+                    help="build the mesh BVHs with the sequential host restatement instead of crt_build_mesh_bvh")
     return ap.parse_args()
 
 
@@ -163,7 +165,8 @@ def main():
     barrier()
     files = assets.scene_files(args.scene)
     t = time.perf_counter()
-    hs = crt_amd.HostScene(files)
+    hs = crt_amd.HostScene(files, build_device=None if args.host_build else local)
+    t_load = time.perf_counter() - t
     ref_scene = hs.upload(local)
     scene = ref_scene
     bvh_desc = "reference (bit-exact)"
@@ -174,8 +177,11 @@ def main():
     t_scene = time.perf_counter() - t
     st = scene.stats()
     counts = hs.counts()
+    setup = {"load_build_upload_s": round(t_scene, 3), "load_and_mesh_bvh_s": round(t_load, 3),
+             "mesh_bvh_build": "host" if args.host_build else "gpu (crt_build_mesh_bvh)",
+             "mesh_bvh_device_ms": round(hs.device_build_ms(), 2)}
     log_r(f"[scene] {args.scene}: {counts['n_indices'] // 3} triangles, {st['device_nodes']} nodes, "
-          f"{st['device_bytes'] / 1e6:.1f} MB in HBM, host load+build+upload {t_scene:.2f}s")
+          f"{st['device_bytes'] / 1e6:.1f} MB in HBM, load+build+upload {t_scene:.2f}s {setup}")
 
     cam = crt_amd.camera(args.spp)
     r = crt_amd.Renderer(W, H, local)
@@ -308,6 +314,7 @@ def main():
             "paths_per_s": round(W * H * args.spp * args.steps / elapsed, 1),
             "render_kernel_ms_avg": round(kernel_ms_avg, 3), "render_kernel_ms_max_over_ranks": round(kernel_ms_max, 3),
             "roofline": roofline, "roofline_valu": roofline_valu, "cpu_baseline": cpu, "parity": parity,
+            "setup": setup,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
