@@ -223,6 +223,13 @@ int  crt_renderer_set_kernel_variant(crt_renderer* r, int variant);
  * frame's kernels have been enqueued AND the queue has drained (host-synchronous). */
 int  crt_renderer_set_wavefront(crt_renderer* r, int refill_lanes, int check_iterations);
 long long crt_renderer_wavefront_iterations(const crt_renderer* r);   /* iterations of the last variant-5 render */
+/* Work order of variants 7 and 8 (4-wide scenes).  Cost probe: before the render, variant 4 traces probe_spp samples
+ * per pixel over the same RNG state without writing anything, and the per-pixel ray counts order the work
+ * most-expensive-first (variant 7: pixels handed to lanes from a global queue; variant 8: 8x8 tiles, one wave per
+ * workgroup).  Renders with fewer than min_spp samples per pixel skip the probe.  xcd_bands (variant 8): each of
+ * the 8 XCDs renders one horizontal strip of the image, so its L2 serves one region.  Default 4, 64, 0;
+ * probe_spp 0 disables the probe.  Results never depend on the order. */
+int  crt_renderer_set_schedule(crt_renderer* r, int probe_spp, int min_spp, int xcd_bands);
 /* Variants 2-4: number of parked lanes (1..64) that triggers a shading/regeneration pass; default 24 for
  * variants 2/3 and 40 for variant 4 (setting it sets both). */
 int  crt_renderer_set_regen_threshold(crt_renderer* r, int lanes);

@@ -96,7 +96,7 @@ HIP_SYMBOLS = [
     "crt_renderer_last_kernel_name",
     "crt_renderer_attach_linear", "crt_renderer_set_kernel_variant", "crt_renderer_get_schedule_stats",
     "crt_renderer_set_regen_threshold", "crt_renderer_set_occupancy_target",
-    "crt_build_mesh_bvh",
+    "crt_build_mesh_bvh", "crt_renderer_set_schedule",
     "crt_selftest_math", "crt_selftest_rng", "crt_selftest_scan", "crt_selftest_rcp",
 ]
 HOST_SYMBOLS = [
@@ -160,6 +160,7 @@ def hip():
             "crt_renderer_get_schedule_stats": ([P, P], i32),
             "crt_renderer_set_regen_threshold": ([P, i32], i32),
             "crt_renderer_set_occupancy_target": ([P, i32], i32),
+            "crt_renderer_set_schedule": ([P, i32, i32], i32),
             "crt_build_mesh_bvh": ([i32, P, C.c_uint32, P, P, C.c_uint32, P, P, P, P], i32),
             "crt_selftest_math": ([P, P, i32, P, P], i32),
             "crt_selftest_rng": ([u64, P, i32, i32, P, P], i32),

@@ -65,6 +65,12 @@ struct RenderParams {
     float* __restrict__ sum;      // W*H*3
     unsigned long long* __restrict__ counters;  // crt_work_counters layout
     crt_camera_desc cam;
+    // variant 7 (persistent, 4-wide scenes): lanes take pixels from a global queue
+    const uint32_t* __restrict__ order;   // slot -> pixel index (most expensive first, from the probe); ~0 = none
+    uint32_t* __restrict__ queue;         // next unclaimed slot
+    int n_slots;
+    int tiles_x;                          // variant 8: 8x8 tiles per row (order[] holds tile indices)
+    uint32_t* __restrict__ probe_cost;    // probe launch (variant 4): rays per pixel; nothing else is written
 };
 
 struct TraceCounts {
@@ -952,13 +958,29 @@ __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int h
 // VARIANT 0: per-lane traversal (leaf loops inside the lane).  VARIANT 1: cooperative leaves.
 // VARIANT 2: cooperative leaves + traversal-step scheduling.  MINW: occupancy target (waves per SIMD)
 // handed to the register allocator through __launch_bounds__.
+#ifdef CRT_PROFILE_WAVE_TIMES
+// Profiling build only (tools/build_profile_lib.sh): per-wave start/end of the last render launch
+// (s_memrealtime, 100 MHz), read with crt_profile_wave_times — the occupancy timeline of the launch.
+__device__ unsigned long long g_wave_prof[2 * 4 * 65536];
+#endif
+
+// Waves per workgroup: 4 (16x16 pixels), or 1 for variant 8 (one 8x8 tile per workgroup, so a finished wave frees
+// its slot at once instead of holding it until its three siblings end).
+template <int VARIANT> struct KernelShape { static constexpr int waves = VARIANT == 8 ? 1 : 4; };
+
 template <bool COUNT, int VARIANT, int MINW>
-__global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
-    __shared__ WaveLds lds[VARIANT >= 1 ? 4 : 1];
+__global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_render_kernel(RenderParams P) {
+#ifdef CRT_PROFILE_WAVE_TIMES
+    const unsigned long long prof_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    constexpr int WGW = KernelShape<VARIANT>::waves;
+    __shared__ WaveLds lds[VARIANT >= 1 ? WGW : 1];
     // variant 4: 16 LDS stack entries per lane at 5 waves/SIMD; 12 at 6+ so 6 workgroups fit the 160 KiB
-    constexpr bool WIDE = VARIANT == 4;
+    constexpr bool PERSIST = VARIANT == 7;
+    constexpr bool TILED = VARIANT == 8;    // variant 4 with one wave per workgroup and a tile order
+    constexpr bool WIDE = VARIANT == 4 || PERSIST || TILED;
     constexpr int SD = WIDE ? (MINW >= 7 ? 11 : MINW >= 6 ? 12 : STACK_LDS) : 1;
-    __shared__ uint32_t stack_lds[WIDE ? 4 * SD * 64 : 1];
+    __shared__ uint32_t stack_lds[WIDE ? WGW * SD * 64 : 1];
     __shared__ float sph_lds[24];
     if (WIDE) {
         if (threadIdx.x < 24) sph_lds[threadIdx.x] = (&P.sph2[0][0])[threadIdx.x];
@@ -967,8 +989,16 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
     // 16x16 pixel tile per workgroup, 8x8 per wave64.
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: LDS bases stay scalar
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    int x, y;
+    if (TILED) {                               // workgroup b renders 8x8 tile order[b]
+        const uint32_t t = P.order ? P.order[blockIdx.x] : blockIdx.x;
+        if (t == 0xffffffffu) return;          // padding slot of the XCD-band order
+        x = (int)(t % (uint32_t)P.tiles_x) * 8 + (lane & 7);
+        y = (int)(t / (uint32_t)P.tiles_x) * 8 + (lane >> 3);
+    } else {
+        x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+        y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    }
     const bool valid = x < P.width && y < P.height;
     const int pix = valid ? y * P.width + x : 0;
 
@@ -977,7 +1007,7 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
     S.pixel = v3(0.f, 0.f, 0.f);
     S.o = v3(0, 0, 0); S.d = v3(0, 0, 1); S.thr = v3(1, 1, 1);
     S.remaining = 0; S.bounce = 0; S.need_new = true; S.rays = 0; S.paths = 0;
-    if (valid) {
+    if (valid && !PERSIST) {
         const uint32_t* r = P.rng + 6 * (size_t)pix;
         S.s.v0 = r[0]; S.s.v1 = r[1]; S.s.v2 = r[2]; S.s.v3 = r[3]; S.s.v4 = r[4]; S.s.d = r[5];
         if (P.accumulate) S.pixel = v3(P.sum[3 * (size_t)pix], P.sum[3 * (size_t)pix + 1], P.sum[3 * (size_t)pix + 2]);
@@ -1004,6 +1034,106 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
             const int hit = trace<COUNT>(P.nodes, P.prims, P.n_nodes, layout_base(S.d, P.n_layouts, P.n_nodes), S.o,
                                          S.d, t, cnt);
             shade(S, P, hit, t);
+        }
+    } else if (PERSIST) {
+        // Variant 4's scheduling, but a lane whose pixel has no samples left stores it and takes the next
+        // pixel slot from the global queue (8x8 tiles in `order`, most expensive first), so lanes never wait
+        // for their wave's slowest pixel and waves never wait for their workgroup or the launch's last tiles.
+        // Each pixel is still traced by ONE lane, samples in order, from its own RNG stream: same results.
+        WaveLds& L = lds[wave];
+        uint32_t* stk = stack_lds + wave * SD * 64;
+        const float INF = __builtin_inff();
+        const size_t n_pix = (size_t)P.width * P.height;
+        const uint32_t total_slots = (uint32_t)P.n_slots;
+        const uint64_t below = (1ull << lane) - 1ull;
+        bool live = false, has_result = false, have = false;
+        int node = -1, sp = 0, hit = -1, px = 0, py = 0, ppix = 0;
+        float closest = INF;
+        V3 inv = v3(0.f, 0.f, 0.f);
+        uint32_t pool = 0, used = 64;    // wave-uniform: first slot of the reserved block, slots handed out
+        bool exhausted = false;
+        L.owner_at[lane] = 0;
+        for (;;) {
+            const bool parked = live && node < 0;
+            const int n_parked = __popcll(__ballot(parked));
+            const int n_live = __popcll(__ballot(live));
+            const uint64_t c0 = COUNT ? shader_clock() : 0;
+            if (n_parked >= P.regen_threshold || n_parked == n_live) {
+                if (COUNT) cnt.passes++;
+                if (parked) {
+                    if (has_result) shade(S, P, hit, closest);
+                    live = next_ray(S, C, px, py, P.max_bounces);
+                    has_result = false;
+                }
+                if (have && !live) {     // the pixel's samples are done: store it (CUDAKernels.h:162-165)
+                    uint32_t* r = P.rng + 6 * (size_t)ppix;
+                    r[0] = S.s.v0; r[1] = S.s.v1; r[2] = S.s.v2; r[3] = S.s.v3; r[4] = S.s.v4; r[5] = S.s.d;
+                    P.sum[3 * (size_t)ppix] = S.pixel.x;
+                    P.sum[3 * (size_t)ppix + 1] = S.pixel.y;
+                    P.sum[3 * (size_t)ppix + 2] = S.pixel.z;
+                    have = false;
+                }
+                while (!exhausted) {     // lanes without a pixel take the next slots
+                    const uint64_t need = __ballot(!have);
+                    if (need == 0) break;
+                    if (used >= 64u) {
+                        uint32_t b = 0;
+                        if (lane == 0) b = atomicAdd(P.queue, 64u);
+                        pool = __builtin_amdgcn_readfirstlane(b);
+                        used = 0;
+                        if (pool >= total_slots) { exhausted = true; break; }
+                    }
+                    const uint32_t take = min((uint32_t)__popcll(need), 64u - used);
+                    const uint32_t rank = (uint32_t)__popcll(need & below);
+                    if (!have && rank < take && pool + used + rank < total_slots) {
+                        const uint32_t pixel = P.order[pool + used + rank];
+                        if (pixel != 0xffffffffu) {
+                            ppix = (int)pixel;
+                            px = ppix % P.width;
+                            py = ppix / P.width;
+                            const uint32_t* r = P.rng + 6 * (size_t)ppix;
+                            S.s.v0 = r[0]; S.s.v1 = r[1]; S.s.v2 = r[2]; S.s.v3 = r[3]; S.s.v4 = r[4]; S.s.d = r[5];
+                            S.pixel = P.accumulate ? v3(P.sum[3 * (size_t)ppix], P.sum[3 * (size_t)ppix + 1],
+                                                        P.sum[3 * (size_t)ppix + 2])
+                                                   : v3(0.f, 0.f, 0.f);
+                            S.remaining = P.spp;
+                            S.need_new = true;
+                            have = true;
+                            live = next_ray(S, C, px, py, P.max_bounces);
+                            if (!live) {         // spp == 0: nothing to trace, store as is
+                                uint32_t* w = P.rng + 6 * (size_t)ppix;
+                                w[0] = S.s.v0; w[1] = S.s.v1; w[2] = S.s.v2; w[3] = S.s.v3; w[4] = S.s.v4; w[5] = S.s.d;
+                                P.sum[3 * (size_t)ppix] = S.pixel.x;
+                                P.sum[3 * (size_t)ppix + 1] = S.pixel.y;
+                                P.sum[3 * (size_t)ppix + 2] = S.pixel.z;
+                                have = false;
+                            }
+                        }
+                    }
+                    used += take;
+                }
+                if (live && node < 0) {          // a new ray: the parked lanes' next ray or a new pixel's first
+                    ++S.rays;
+                    has_result = true;
+                    node = 0;
+                    sp = 0;
+                    closest = INF;
+                    hit = -1;
+#ifdef CRT_INV_IEEE
+                    inv = v3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
+#else
+                    inv = v3(recip_exact_any(S.d.x), recip_exact_any(S.d.y), recip_exact_any(S.d.z));
+#endif
+                    ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d, inv,
+                                closest, hit, sph_lds);
+                    if (COUNT) cnt.spheres += P.n_ray_spheres;
+                    L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
+                    if (COUNT) cnt.trace_calls++;
+                }
+                if (!__ballot(live)) break;      // the queue is empty and every lane is done
+            }
+            if (COUNT) cnt.cyc_regen += shader_clock() - c0;
+            traverse_step4<COUNT>(P, S.o, S.d, inv, node, sp, closest, hit, cnt, L, stk, lane, (size_t)ppix, n_pix);
         }
     } else if (WIDE) {
         // Same scheduling as variant 3 over a 4-wide BVH: node < 0 = no node left (lane parked).
@@ -1118,7 +1248,11 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
         }
     }
 
-    if (valid) {
+    if (WIDE && !PERSIST && P.probe_cost) {   // probe launch: rays of this pixel; no state is written
+        if (valid) P.probe_cost[pix] = S.rays;
+        return;
+    }
+    if (valid && !PERSIST) {
         uint32_t* r = P.rng + 6 * (size_t)pix;
         r[0] = S.s.v0; r[1] = S.s.v1; r[2] = S.s.v2; r[3] = S.s.v3; r[4] = S.s.v4; r[5] = S.s.d;
         P.sum[3 * (size_t)pix] = S.pixel.x;
@@ -1148,6 +1282,15 @@ __global__ __launch_bounds__(256, MINW) void crt_render_kernel(RenderParams P) {
         }
     }
     if (lane == 0) atomicAdd(&P.counters[0], (unsigned long long)wr);
+#ifdef CRT_PROFILE_WAVE_TIMES
+    {
+        const unsigned wid = (blockIdx.y * gridDim.x + blockIdx.x) * (unsigned)WGW + (threadIdx.x >> 6);
+        if (lane == 0 && wid < 4u * 65536u) {
+            g_wave_prof[2 * wid] = prof_t0;
+            g_wave_prof[2 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+#endif
 #ifdef CRT_NODE_PREFETCH
     if (cnt.pf0 == 1.5e-38f && cnt.pf1 == -1.5e-38f) atomicOr(P.err, 0u);   // keeps the prefetch loads
 #endif
@@ -1565,6 +1708,92 @@ __global__ void crt_selftest_rng_kernel(const uint32_t* st_in, int n, int n_draw
     if (i >= n) return;
     Rng s{st_in[6 * i], st_in[6 * i + 1], st_in[6 * i + 2], st_in[6 * i + 3], st_in[6 * i + 4], st_in[6 * i + 5]};
     for (int k = 0; k < n_draw; ++k) out[(size_t)i * n_draw + k] = uniform(s);
+}
+
+// ------------------------------------------------------------------ variant 7: pixel order from the probe
+// Most expensive pixels first (longest-processing-time order), so the pixels whose sample sequences take
+// longest start at once and the launch ends on cheap ones.  Counting sort of the probe's per-pixel ray
+// counts (keys clamped to 1023), descending; within a key the order is arbitrary (scheduling only).
+constexpr int ORDER_KEYS = 1024;
+constexpr int ORDER_ITEMS = 1024;   // pixels per workgroup of the sort passes
+__device__ __forceinline__ uint32_t order_bucket(uint32_t cost) { return ORDER_KEYS - 1 - min(cost, (uint32_t)ORDER_KEYS - 1); }
+__global__ __launch_bounds__(256) void crt_order_hist_kernel(const uint32_t* __restrict__ cost, int n,
+                                                             uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[ORDER_KEYS];
+    for (int i = threadIdx.x; i < ORDER_KEYS; i += 256) h[i] = 0;
+    __syncthreads();
+    const int b0 = blockIdx.x * ORDER_ITEMS;
+    for (int i = b0 + threadIdx.x; i < min(n, b0 + ORDER_ITEMS); i += 256) atomicAdd(&h[order_bucket(cost[i])], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < ORDER_KEYS; i += 256)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+__global__ __launch_bounds__(ORDER_KEYS) void crt_order_scan_kernel(uint32_t* __restrict__ hist) {
+    __shared__ uint32_t part[ORDER_KEYS];
+    const int t = threadIdx.x;
+    const uint32_t c = hist[t];
+    part[t] = c;
+    __syncthreads();
+    for (int o = 1; o < ORDER_KEYS; o <<= 1) {
+        const uint32_t add = t >= o ? part[t - o] : 0u;
+        __syncthreads();
+        part[t] += add;
+        __syncthreads();
+    }
+    hist[t] = part[t] - c;   // exclusive offsets
+}
+__global__ __launch_bounds__(256) void crt_order_scatter_kernel(const uint32_t* __restrict__ cost, int n,
+                                                                uint32_t* __restrict__ hist,
+                                                                uint32_t* __restrict__ order, uint32_t base) {
+    __shared__ uint32_t h[ORDER_KEYS];
+    for (int i = threadIdx.x; i < ORDER_KEYS; i += 256) h[i] = 0;
+    __syncthreads();
+    const int b0 = blockIdx.x * ORDER_ITEMS;
+    uint32_t rank[ORDER_ITEMS / 256];
+    for (int k = 0; k < ORDER_ITEMS / 256; ++k) {
+        const int i = b0 + threadIdx.x + 256 * k;
+        rank[k] = i < n ? atomicAdd(&h[order_bucket(cost[i])], 1u) : 0u;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < ORDER_KEYS; i += 256)   // reserve this block's run of every key
+        if (h[i]) h[i] = atomicAdd(&hist[i], h[i]);
+    __syncthreads();
+    for (int k = 0; k < ORDER_ITEMS / 256; ++k) {
+        const int i = b0 + threadIdx.x + 256 * k;
+        if (i < n) order[h[order_bucket(cost[i])] + rank[k]] = base + (uint32_t)i;
+    }
+}
+// Variant 8: the key of an 8x8 tile is its most expensive pixel (the wave ends with its slowest lane).
+__global__ void crt_tile_cost_kernel(const uint32_t* __restrict__ pix_cost, int width, int height, int tiles_x,
+                                     int n_tiles, uint32_t* __restrict__ tile_cost) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_tiles) return;
+    const int x0 = (t % tiles_x) * 8, y0 = (t / tiles_x) * 8;
+    uint32_t m = 0;
+    for (int y = y0; y < min(height, y0 + 8); ++y)
+        for (int x = x0; x < min(width, x0 + 8); ++x) m = max(m, pix_cost[(size_t)y * width + x]);
+    tile_cost[t] = m;
+}
+
+// Variant 8, XCD bands: workgroups are dealt round-robin over the 8 XCDs, so workgroup b runs on the XCD of
+// b % 8.  Band k (tiles [k*per, (k+1)*per) in row order, a horizontal strip of the image) goes to workgroups
+// b % 8 == k, in the order `sorted` holds it, so each XCD's L2 serves one strip.
+__global__ void crt_order_bands_kernel(const uint32_t* __restrict__ sorted, int n_tiles, int per,
+                                       uint32_t* __restrict__ order) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= 8 * per) return;
+    const int k = b % 8, j = b / 8, t = k * per + j;
+    order[b] = (j < per && t < n_tiles) ? (sorted ? sorted[t] : (uint32_t)t) : 0xffffffffu;
+}
+
+// No probe: 8x8 tiles in row order, pixels row-major inside a tile (a wave's first 64 slots are one tile, so
+// its primary rays are coherent); slots of partial edge tiles hold ~0.
+__global__ void crt_order_tiles_kernel(uint32_t* __restrict__ order, int width, int height, int n_slots) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_slots) return;
+    const int tiles_x = (width + 7) / 8, tile = s >> 6, q = s & 63;
+    const int x = (tile % tiles_x) * 8 + (q & 7), y = (tile / tiles_x) * 8 + (q >> 3);
+    order[s] = (x < width && y < height) ? (uint32_t)(y * width + x) : 0xffffffffu;
 }
 
 // ------------------------------------------------------------------ host side
@@ -1985,6 +2214,17 @@ struct crt_renderer {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     char kernel_name[64] = "";     // instantiation of the last render launch, rocprof's spelling
+    // variant 7: pixel order, slot queue, probe costs, sort scratch (allocated on first use)
+    uint32_t* d_order = nullptr;
+    uint32_t* d_queue = nullptr;
+    uint32_t* d_tile_cost = nullptr;   // per-pixel probe costs
+    uint32_t* d_order_hist = nullptr;
+    uint32_t* d_tile_key = nullptr;    // variant 8: per-tile keys
+    int probe_spp = 4;             // samples per pixel of the cost probe (0 = no probe: 8x8-tile order)
+    int probe_min_spp = 64;        // renders with fewer samples per pixel skip the probe
+    int xcd_bands = 0;             // variant 8: each XCD renders one horizontal strip (see crt_order_bands_kernel)
+    uint32_t* d_sorted = nullptr;  // variant 8: tiles sorted per band
+    int n_cus = 0;
     int variant = 3;               // see crt_renderer_set_kernel_variant
     unsigned long long diag[3] = {0, 0, 0};
     unsigned long long prof[7] = {0, 0, 0, 0, 0, 0, 0};   // COUNT-mode section profile (variant 4)
@@ -2287,6 +2527,12 @@ void crt_renderer_destroy(crt_renderer* R) {
     if (R->d_seq) (void)hipFree(R->d_seq);
     if (R->d_counters) (void)hipFree(R->d_counters);
     if (R->d_ovf) (void)hipFree(R->d_ovf);
+    if (R->d_order) (void)hipFree(R->d_order);
+    if (R->d_queue) (void)hipFree(R->d_queue);
+    if (R->d_tile_cost) (void)hipFree(R->d_tile_cost);
+    if (R->d_order_hist) (void)hipFree(R->d_order_hist);
+    if (R->d_tile_key) (void)hipFree(R->d_tile_key);
+    if (R->d_sorted) (void)hipFree(R->d_sorted);
     if (R->d_wf_ray) (void)hipFree(R->d_wf_ray);
     if (R->d_wf_path) (void)hipFree(R->d_wf_path);
     if (R->d_wf_rem) (void)hipFree(R->d_wf_rem);
@@ -2309,8 +2555,16 @@ int crt_renderer_init_rand(crt_renderer* R, unsigned long long seed, unsigned lo
 }
 
 int crt_renderer_set_kernel_variant(crt_renderer* R, int variant) {
-    if (!R || variant < 0 || variant > 5) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant");
+    if (!R || variant < 0 || variant > 8 || variant == 6) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant");
     R->variant = variant;
+    return CRT_OK;
+}
+
+int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int xcd_bands) {
+    if (!R || probe_spp < 0 || probe_spp > 64 || min_spp < 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad schedule");
+    R->probe_spp = probe_spp;
+    R->probe_min_spp = min_spp;
+    R->xcd_bands = xcd_bands ? 1 : 0;
     return CRT_OK;
 }
 
@@ -2426,7 +2680,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     HIP_TRY(hipSetDevice(R->device));
     hipStream_t st = (hipStream_t)stream;
     HIP_TRY(hipMemsetAsync(R->d_counters, 0, 16 * sizeof(unsigned long long), st));
-    RenderParams P;
+    RenderParams P{};
     P.nodes = S->d_nodes; P.prims = S->d_prims; P.mats = S->d_mats; P.shade = S->d_shade;
     P.n_nodes = S->n_nodes; P.n_mats = S->n_mats; P.n_prims = S->n_prims; P.n_layouts = S->layouts;
     P.err = reinterpret_cast<unsigned*>(R->d_counters + 7);
@@ -2434,6 +2688,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.accumulate = (flags & CRT_RENDER_ACCUMULATE) ? 1 : 0;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     P.ovf = nullptr;
+    P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0;
     P.stack_cap = S->stack_cap;
     P.sphere_first = S->sphere_first;
     P.n_ray_spheres = S->n_ray_spheres;
@@ -2486,7 +2741,131 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, V, W>), grid, block, 0, st, P);  \
         else hipLaunchKernelGGL((crt_render_kernel<false, V, W>), grid, block, 0, st, P);     \
     } while (0)
-    if (S->width == 4) {
+    if (S->width == 4 && R->variant == 8) {
+        const size_t n_pix = (size_t)R->width * R->height;
+        const int tiles_x = (R->width + 7) / 8, n_tiles = tiles_x * ((R->height + 7) / 8);
+        if (!R->d_tile_key) {
+            HIP_TRY(hipStreamSynchronize(st));
+            if (!R->d_order) {
+                HIP_TRY(hipMalloc((void**)&R->d_order, std::max(n_pix, (size_t)n_tiles * 64) * 4));
+                HIP_TRY(hipMalloc((void**)&R->d_queue, 4));
+                HIP_TRY(hipMalloc((void**)&R->d_tile_cost, n_pix * 4));
+                HIP_TRY(hipMalloc((void**)&R->d_order_hist, ORDER_KEYS * 4));
+                HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
+            }
+            HIP_TRY(hipMalloc((void**)&R->d_tile_key, (size_t)n_tiles * 4));
+        }
+        P.tiles_x = tiles_x;
+        P.order = nullptr;
+        const int per = (n_tiles + 7) / 8;
+        const bool probe = R->probe_spp > 0 && spp >= R->probe_min_spp;
+        if (probe) {
+            // cost probe (variant 4, read-only) -> slowest pixel per tile -> tiles most expensive first (per XCD
+            // band when banded)
+            RenderParams Q = P;
+            Q.spp = R->probe_spp;
+            Q.accumulate = 0;
+            Q.probe_cost = R->d_tile_cost;
+            if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<false, 4, 6>), grid, block, 0, st, Q);
+            else hipLaunchKernelGGL((crt_render_kernel<false, 4, 5>), grid, block, 0, st, Q);
+            hipLaunchKernelGGL(crt_tile_cost_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_tile_cost,
+                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key);
+            uint32_t* sorted = R->xcd_bands ? R->d_sorted : R->d_order;
+            if (R->xcd_bands && !sorted) {
+                HIP_TRY(hipStreamSynchronize(st));
+                HIP_TRY(hipMalloc((void**)&R->d_sorted, (size_t)n_tiles * 4));
+                sorted = R->d_sorted;
+            }
+            const int n_seg = R->xcd_bands ? 8 : 1, seg = R->xcd_bands ? per : n_tiles;
+            for (int k = 0; k < n_seg; ++k) {
+                const int b0 = k * seg, n = std::min(n_tiles, b0 + seg) - b0;
+                if (n <= 0) break;
+                const unsigned ob = (unsigned)((n + ORDER_ITEMS - 1) / ORDER_ITEMS);
+                HIP_TRY(hipMemsetAsync(R->d_order_hist, 0, ORDER_KEYS * 4, st));
+                hipLaunchKernelGGL(crt_order_hist_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key + b0, n, R->d_order_hist);
+                hipLaunchKernelGGL(crt_order_scan_kernel, dim3(1), dim3(ORDER_KEYS), 0, st, R->d_order_hist);
+                hipLaunchKernelGGL(crt_order_scatter_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key + b0, n,
+                                   R->d_order_hist, sorted + b0, (uint32_t)b0);
+            }
+            if (R->xcd_bands)
+                hipLaunchKernelGGL(crt_order_bands_kernel, dim3((8 * per + 255) / 256), dim3(256), 0, st, sorted,
+                                   n_tiles, per, R->d_order);
+            P.order = R->d_order;
+        } else if (R->xcd_bands) {
+            hipLaunchKernelGGL(crt_order_bands_kernel, dim3((8 * per + 255) / 256), dim3(256), 0, st, nullptr, n_tiles,
+                               per, R->d_order);
+            P.order = R->d_order;
+        }
+        const int n_wg = R->xcd_bands ? 8 * per : n_tiles;
+        const dim3 tgrid(n_wg), tblock(64);
+        const char* cs = cnt ? "true" : "false";
+        if (occ >= 7) {
+            std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 8, 7>", cs);
+            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 8, 7>), tgrid, tblock, 0, st, P);
+            else hipLaunchKernelGGL((crt_render_kernel<false, 8, 7>), tgrid, tblock, 0, st, P);
+        } else if (occ >= 6) {
+            std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 8, 6>", cs);
+            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 8, 6>), tgrid, tblock, 0, st, P);
+            else hipLaunchKernelGGL((crt_render_kernel<false, 8, 6>), tgrid, tblock, 0, st, P);
+        } else {
+            std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 8, 5>", cs);
+            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 8, 5>), tgrid, tblock, 0, st, P);
+            else hipLaunchKernelGGL((crt_render_kernel<false, 8, 5>), tgrid, tblock, 0, st, P);
+        }
+    } else if (S->width == 4 && R->variant == 7) {
+        const size_t n_pix = (size_t)R->width * R->height;
+        const int tiles_x = (R->width + 7) / 8, tiles_y = (R->height + 7) / 8;
+        const size_t n_tile_slots = (size_t)tiles_x * tiles_y * 64;
+        const size_t cap = std::max(n_pix, n_tile_slots);
+        if (!R->d_order) {
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipMalloc((void**)&R->d_order, cap * 4));
+            HIP_TRY(hipMalloc((void**)&R->d_queue, 4));
+            HIP_TRY(hipMalloc((void**)&R->d_tile_cost, n_pix * 4));
+            HIP_TRY(hipMalloc((void**)&R->d_order_hist, ORDER_KEYS * 4));
+            HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
+        }
+        if (R->probe_spp > 0 && spp >= R->probe_min_spp) {
+            // cost probe: variant 4 at probe_spp samples over the same RNG state, read-only: rays per pixel
+            RenderParams Q = P;
+            Q.spp = R->probe_spp;
+            Q.accumulate = 0;
+            Q.probe_cost = R->d_tile_cost;
+            if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<false, 4, 6>), grid, block, 0, st, Q);
+            else hipLaunchKernelGGL((crt_render_kernel<false, 4, 5>), grid, block, 0, st, Q);
+            const unsigned ob = (unsigned)((n_pix + ORDER_ITEMS - 1) / ORDER_ITEMS);
+            HIP_TRY(hipMemsetAsync(R->d_order_hist, 0, ORDER_KEYS * 4, st));
+            hipLaunchKernelGGL(crt_order_hist_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_cost, (int)n_pix, R->d_order_hist);
+            hipLaunchKernelGGL(crt_order_scan_kernel, dim3(1), dim3(ORDER_KEYS), 0, st, R->d_order_hist);
+            hipLaunchKernelGGL(crt_order_scatter_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_cost, (int)n_pix,
+                               R->d_order_hist, R->d_order, 0u);
+            P.n_slots = (int)n_pix;
+        } else {
+            hipLaunchKernelGGL(crt_order_tiles_kernel, dim3((unsigned)((n_tile_slots + 255) / 256)), dim3(256), 0, st,
+                               R->d_order, R->width, R->height, (int)n_tile_slots);
+            P.n_slots = (int)n_tile_slots;
+        }
+        HIP_TRY(hipMemsetAsync(R->d_queue, 0, 4, st));
+        P.order = R->d_order;
+        P.queue = R->d_queue;
+        P.probe_cost = nullptr;
+        const int per_cu = occ >= 7 ? 7 : occ >= 6 ? 6 : 5;        // workgroups of 4 waves resident per CU
+        const int n_wg = std::max(1, std::min(R->n_cus * per_cu, (int)((n_pix + 255) / 256)));
+        const dim3 pgrid(n_wg);
+        if (occ >= 7) {
+            std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 7, 7>", cnt ? "true" : "false");
+            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 7, 7>), pgrid, block, 0, st, P);
+            else hipLaunchKernelGGL((crt_render_kernel<false, 7, 7>), pgrid, block, 0, st, P);
+        } else if (occ >= 6) {
+            std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 7, 6>", cnt ? "true" : "false");
+            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 7, 6>), pgrid, block, 0, st, P);
+            else hipLaunchKernelGGL((crt_render_kernel<false, 7, 6>), pgrid, block, 0, st, P);
+        } else {
+            std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 7, 5>", cnt ? "true" : "false");
+            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 7, 5>), pgrid, block, 0, st, P);
+            else hipLaunchKernelGGL((crt_render_kernel<false, 7, 5>), pgrid, block, 0, st, P);
+        }
+    } else if (S->width == 4) {
         if (occ >= 7) CRT_LAUNCH(4, 7);
         else if (occ >= 6) CRT_LAUNCH(4, 6);
         else if (occ >= 5) CRT_LAUNCH(4, 5);
@@ -2528,7 +2907,7 @@ int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene*
     if (spp < 0 || max_bounces < 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "negative spp / bounces");
     HIP_TRY(hipSetDevice(R->device));
     HIP_TRY(hipMemset(R->d_counters, 0, 16 * sizeof(unsigned long long)));
-    CompareParams Q;
+    CompareParams Q{};
     RenderParams& P = Q.A;
     P.nodes = A->d_nodes; P.prims = A->d_prims; P.mats = A->d_mats; P.shade = A->d_shade;
     P.n_nodes = A->n_nodes; P.n_mats = A->n_mats; P.n_prims = A->n_prims; P.n_layouts = A->layouts;
@@ -2640,6 +3019,15 @@ uint8_t* crt_renderer_rgba_device_ptr(crt_renderer* R) { return R ? R->d_rgba : 
 uint32_t* crt_renderer_rng_device_ptr(crt_renderer* R) { return R ? R->d_rng : nullptr; }
 
 const char* crt_renderer_last_kernel_name(const crt_renderer* R) { return R ? R->kernel_name : ""; }
+
+#ifdef CRT_PROFILE_WAVE_TIMES
+extern "C" int crt_profile_wave_times(unsigned long long* out, int n_waves) {
+    if (!out || n_waves <= 0 || n_waves > 4 * 65536) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_prof), (size_t)n_waves * 16, 0, hipMemcpyDeviceToHost));
+    return CRT_OK;
+}
+#endif
 
 float crt_renderer_last_kernel_ms(crt_renderer* R) {
     if (!R || !R->timed) return -1.f;

@@ -167,3 +167,64 @@ def test_wavefront_equals_megakernel(rebuilt, refill):
     assert np.array_equal(a.linear().view(np.uint32), c.linear().view(np.uint32))
     assert c.counters()["rays"] == a.counters()["rays"]
 
+
+
+@pytest.mark.parametrize("variant", [7, 8])
+@pytest.mark.parametrize("w,h,spp", [(160, 90, 8), (100, 37, 70), (64, 36, 0)])
+def test_persistent_queue_variant_is_bit_identical(rebuilt, w, h, spp, variant):
+    """Variants 7 (lanes take pixels from a global queue in probe-cost order) and 8 (one wave per workgroup, 8x8
+    tiles in probe-cost order) trace every pixel with ONE lane, samples in order, from its own RNG stream: the
+    frame, the RNG state and the ray count equal variant 4's.  spp 70 >= 64 runs the cost probe and the sorted
+    order; 8 uses row-major order; 0 traces nothing.  100x37 has partial 8x8 tiles."""
+    dev = rebuilt["cornell_bunny", "w4"]
+    cam = crt_amd.camera(max(spp, 1))
+    a = _frame(dev, w, h, spp, 20, cam, variant=4)
+    b = _frame(dev, w, h, spp, 20, cam, variant=variant)
+    assert np.array_equal(a.linear().view(np.uint32), b.linear().view(np.uint32))
+    assert np.array_equal(a.rgba8(), b.rgba8())
+    assert np.array_equal(a.rng_state(), b.rng_state())
+    assert a.counters()["rays"] == b.counters()["rays"]
+    # accumulate continues every pixel's sum and stream
+    for r in (a, b):
+        r.render(dev, 3, 20, accumulate=True)
+        r.synchronize()
+    assert np.array_equal(a.linear().view(np.uint32), b.linear().view(np.uint32))
+    assert np.array_equal(a.rng_state(), b.rng_state())
+
+
+@pytest.mark.parametrize("variant", [7, 8])
+def test_persistent_queue_counting_kernel(rebuilt, variant):
+    dev = rebuilt["cornell_bunny", "w4"]
+    cam = crt_amd.camera(4)
+    a = crt_amd.Renderer(96, 54)
+    b = crt_amd.Renderer(96, 54)
+    b.set_kernel_variant(variant)
+    for r in (a, b):
+        r.set_camera(cam)
+        r.init_rand(41)
+        r.render(dev, 4, 20, count_work=True)
+        r.synchronize()
+    ca, cb = a.counters(), b.counters()
+    for k in ("rays", "box_tests", "tri_tests", "sphere_tests", "paths"):
+        assert ca[k] == cb[k], k
+    assert np.array_equal(a.linear().view(np.uint32), b.linear().view(np.uint32))
+    assert b.last_kernel_name() == f"crt_render_kernel<true, {variant}, 6>"
+
+
+@pytest.mark.parametrize("probe_spp", [0, 4])
+def test_xcd_band_order_is_bit_identical(rebuilt, probe_spp):
+    """Variant 8 with the XCD-band work order (each XCD one horizontal strip; padding slots for a tile count
+    that is not a multiple of 8), with and without the cost probe: the same frame as variant 4."""
+    dev = rebuilt["cornell_bunny", "w4"]
+    w, h, spp = 104, 45, 64          # 13 x 6 = 78 tiles: bands of 10, the last two short
+    cam = crt_amd.camera(spp)
+    a = _frame(dev, w, h, spp, 20, cam, variant=4)
+    b = crt_amd.Renderer(w, h)
+    b.set_kernel_variant(8)
+    b.set_schedule(probe_spp, 64, True)
+    b.set_camera(cam)
+    b.init_rand(41)
+    b.render(dev, spp, 20)
+    b.synchronize()
+    assert np.array_equal(a.linear().view(np.uint32), b.linear().view(np.uint32))
+    assert np.array_equal(a.rng_state(), b.rng_state())

@@ -9,6 +9,6 @@ mkdir -p $out
 cd $R/raytracer-cuda_amd
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
   -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-result -munsafe-fp-atomics -fno-slp-vectorize "$@" \
-  -I../include -Icsrc -Ihost -shared -o $out/libcrt_hip.so -x hip csrc/crt_hip.hip \
+  -I../include -Icsrc -Ihost -shared -o $out/libcrt_hip.so -x hip csrc/crt_hip.hip csrc/crt_bvh_build.hip \
   -Wl,-soname,libcrt_hip.so -Wl,--version-script=csrc/exports.map
 echo $out/libcrt_hip.so
