@@ -231,10 +231,10 @@ def main():
         r.synchronize()
         work = r.counters()
         assert work["rays"] == rays_rank, "counting kernel disagrees with the timed kernel"
-    if st.get("width") == 4:
-        variant = 4
-    else:
-        variant = args.kernel_variant if args.kernel_variant is not None else 3
+    try:   # the variant the timed frames ran, from the instantiation name "crt_render_kernel<false, V, W>"
+        variant = int(kname.split(",")[1])
+    except (IndexError, ValueError):
+        variant = args.kernel_variant
     if work is not None:
         bytes_launch = (B_BOX * work["box_tests"] + B_TRI * work["tri_tests"] + B_SPHERE * work["sphere_tests"]
                         + B_RAY * work["rays"] + B_PIXEL * W * H)

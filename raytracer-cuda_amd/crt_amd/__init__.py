@@ -211,9 +211,9 @@ class Renderer:
     def init_rand(self, seed: int = 41, subsequence_base: int = 0, stream=None):
         check(_lib.hip().crt_renderer_init_rand(self.h, int(seed), int(subsequence_base), stream), "init_rand")
 
-    def set_schedule(self, probe_spp: int = 4, min_spp: int = 64, xcd_bands: bool = False):
-        check(_lib.hip().crt_renderer_set_schedule(self.h, int(probe_spp), int(min_spp), int(bool(xcd_bands))),
-              "set_schedule")
+    def set_schedule(self, probe_spp: int = 4, min_spp: int = 64, xcd_bands: bool = False, first_block: bool = False):
+        flags = (1 if xcd_bands else 0) | (2 if first_block else 0)
+        check(_lib.hip().crt_renderer_set_schedule(self.h, int(probe_spp), int(min_spp), flags), "set_schedule")
 
     def set_kernel_variant(self, variant: int):
         check(_lib.hip().crt_renderer_set_kernel_variant(self.h, int(variant)), "set_kernel_variant")

@@ -70,6 +70,7 @@ struct RenderParams {
     uint32_t* __restrict__ queue;         // next unclaimed slot
     int n_slots;
     int tiles_x;                          // variant 8: 8x8 tiles per row (order[] holds tile indices)
+    int first_block_exclusive;            // variant 7: a wave refills lanes only after its first 64 pixels are done
     uint32_t* __restrict__ probe_cost;    // probe launch (variant 4): rays per pixel; nothing else is written
 };
 
@@ -1052,6 +1053,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         V3 inv = v3(0.f, 0.f, 0.f);
         uint32_t pool = 0, used = 64;    // wave-uniform: first slot of the reserved block, slots handed out
         bool exhausted = false;
+        // first_block_exclusive: the wave's first 64 pixels (the most expensive, in probe order) run without
+        // refills, so their slow lanes end in an emptying wave (variant 4's behaviour); afterwards lanes refill
+        int fb = P.first_block_exclusive ? 0 : 2;   // 0: nothing assigned yet, 1: first block running, 2: refill
         L.owner_at[lane] = 0;
         for (;;) {
             const bool parked = live && node < 0;
@@ -1073,7 +1077,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     P.sum[3 * (size_t)ppix + 2] = S.pixel.z;
                     have = false;
                 }
-                while (!exhausted) {     // lanes without a pixel take the next slots
+                if (fb == 1 && !__ballot(have)) fb = 2;   // the first block is done: refill from now on
+                while (!exhausted && fb != 1) {     // lanes without a pixel take the next slots
                     const uint64_t need = __ballot(!have);
                     if (need == 0) break;
                     if (used >= 64u) {
@@ -1112,6 +1117,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     }
                     used += take;
                 }
+                if (fb == 0) fb = 1;
                 if (live && node < 0) {          // a new ray: the parked lanes' next ray or a new pixel's first
                     ++S.rays;
                     has_result = true;
@@ -1248,8 +1254,10 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         }
     }
 
-    if (WIDE && !PERSIST && P.probe_cost) {   // probe launch: rays of this pixel; no state is written
-        if (valid) P.probe_cost[pix] = S.rays;
+    if (WIDE && !PERSIST && P.probe_cost) {   // probe launch: work of this pixel; no state is written
+        // counting probe: a ray's shading + generation costs about as much as 16 child-box tests, a triangle
+        // test about 4 (section profile, profiles/r01h); plain probe: rays
+        if (valid) P.probe_cost[pix] = COUNT ? (16u * S.rays + cnt.boxes + 4u * cnt.tris) >> 3 : S.rays;
         return;
     }
     if (valid && !PERSIST) {
@@ -2223,6 +2231,7 @@ struct crt_renderer {
     int probe_spp = 4;             // samples per pixel of the cost probe (0 = no probe: 8x8-tile order)
     int probe_min_spp = 64;        // renders with fewer samples per pixel skip the probe
     int xcd_bands = 0;             // variant 8: each XCD renders one horizontal strip (see crt_order_bands_kernel)
+    int first_block_exclusive = 0; // variant 7: see RenderParams::first_block_exclusive
     uint32_t* d_sorted = nullptr;  // variant 8: tiles sorted per band
     int n_cus = 0;
     int variant = 3;               // see crt_renderer_set_kernel_variant
@@ -2560,11 +2569,12 @@ int crt_renderer_set_kernel_variant(crt_renderer* R, int variant) {
     return CRT_OK;
 }
 
-int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int xcd_bands) {
+int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int flags) {
     if (!R || probe_spp < 0 || probe_spp > 64 || min_spp < 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad schedule");
     R->probe_spp = probe_spp;
     R->probe_min_spp = min_spp;
-    R->xcd_bands = xcd_bands ? 1 : 0;
+    R->xcd_bands = (flags & 1) ? 1 : 0;
+    R->first_block_exclusive = (flags & 2) ? 1 : 0;
     return CRT_OK;
 }
 
@@ -2741,7 +2751,13 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, V, W>), grid, block, 0, st, P);  \
         else hipLaunchKernelGGL((crt_render_kernel<false, V, W>), grid, block, 0, st, P);     \
     } while (0)
-    if (S->width == 4 && R->variant == 8) {
+    // 4-wide scenes: variant 4 / 5 / 7 / 8 when selected explicitly; otherwise the measured best (profiles/r01w):
+    // 8 (probe-ordered tiles, one wave per workgroup) when the render runs the cost probe, 7 (lanes refill from a
+    // pixel queue) for short renders such as the 1-spp interactive frames
+    int wv = R->variant;
+    if (S->width == 4 && wv != 4 && wv != 5 && wv != 7 && wv != 8)
+        wv = (R->probe_spp > 0 && spp >= R->probe_min_spp) ? 8 : 7;
+    if (S->width == 4 && wv == 8) {
         const size_t n_pix = (size_t)R->width * R->height;
         const int tiles_x = (R->width + 7) / 8, n_tiles = tiles_x * ((R->height + 7) / 8);
         if (!R->d_tile_key) {
@@ -2766,8 +2782,8 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             Q.spp = R->probe_spp;
             Q.accumulate = 0;
             Q.probe_cost = R->d_tile_cost;
-            if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<false, 4, 6>), grid, block, 0, st, Q);
-            else hipLaunchKernelGGL((crt_render_kernel<false, 4, 5>), grid, block, 0, st, Q);
+            if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<true, 4, 6>), grid, block, 0, st, Q);
+            else hipLaunchKernelGGL((crt_render_kernel<true, 4, 5>), grid, block, 0, st, Q);
             hipLaunchKernelGGL(crt_tile_cost_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_tile_cost,
                                R->width, R->height, tiles_x, n_tiles, R->d_tile_key);
             uint32_t* sorted = R->xcd_bands ? R->d_sorted : R->d_order;
@@ -2812,7 +2828,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 8, 5>), tgrid, tblock, 0, st, P);
             else hipLaunchKernelGGL((crt_render_kernel<false, 8, 5>), tgrid, tblock, 0, st, P);
         }
-    } else if (S->width == 4 && R->variant == 7) {
+    } else if (S->width == 4 && wv == 7) {
         const size_t n_pix = (size_t)R->width * R->height;
         const int tiles_x = (R->width + 7) / 8, tiles_y = (R->height + 7) / 8;
         const size_t n_tile_slots = (size_t)tiles_x * tiles_y * 64;
@@ -2849,6 +2865,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         P.order = R->d_order;
         P.queue = R->d_queue;
         P.probe_cost = nullptr;
+        P.first_block_exclusive = R->first_block_exclusive;
         const int per_cu = occ >= 7 ? 7 : occ >= 6 ? 6 : 5;        // workgroups of 4 waves resident per CU
         const int n_wg = std::max(1, std::min(R->n_cus * per_cu, (int)((n_pix + 255) / 256)));
         const dim3 pgrid(n_wg);

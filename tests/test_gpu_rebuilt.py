@@ -214,14 +214,25 @@ def test_persistent_queue_counting_kernel(rebuilt, variant):
 @pytest.mark.parametrize("probe_spp", [0, 4])
 def test_xcd_band_order_is_bit_identical(rebuilt, probe_spp):
     """Variant 8 with the XCD-band work order (each XCD one horizontal strip; padding slots for a tile count
-    that is not a multiple of 8), with and without the cost probe: the same frame as variant 4."""
+    that is not a multiple of 8)."""
+    _schedule_case(rebuilt, 8, probe_spp, xcd_bands=True)
+
+
+@pytest.mark.parametrize("probe_spp", [0, 4])
+def test_first_block_exclusive_is_bit_identical(rebuilt, probe_spp):
+    """Variant 7 whose waves refill only after their first 64 pixels are done."""
+    _schedule_case(rebuilt, 7, probe_spp, first_block=True)
+
+
+def _schedule_case(rebuilt, variant, probe_spp, **flags):
+    """A schedule option, with and without the cost probe: the same frame and RNG state as variant 4."""
     dev = rebuilt["cornell_bunny", "w4"]
     w, h, spp = 104, 45, 64          # 13 x 6 = 78 tiles: bands of 10, the last two short
     cam = crt_amd.camera(spp)
     a = _frame(dev, w, h, spp, 20, cam, variant=4)
     b = crt_amd.Renderer(w, h)
-    b.set_kernel_variant(8)
-    b.set_schedule(probe_spp, 64, True)
+    b.set_kernel_variant(variant)
+    b.set_schedule(probe_spp, 64, **flags)
     b.set_camera(cam)
     b.init_rand(41)
     b.render(dev, spp, 20)
