@@ -68,7 +68,8 @@ def parse():
     ap.add_argument("--traversal-cost", type=float, default=2.0)
     ap.add_argument("--no-parity", action="store_true", help="skip the reference-BVH parity frame")
     ap.add_argument("--host-build", action="store_true",
-                    help="build the mesh BVHs with the sequential host restatement instead of crt_build_mesh_bvh")
+                    help="build the BVHs on the host (mesh: the sequential restatement of the reference builder; "
+                         "rebuilt tree: crt_sah.h) instead of on the GPU")
     return ap.parse_args()
 
 
@@ -172,13 +173,14 @@ def main():
     bvh_desc = "reference (bit-exact)"
     if args.bvh == "rebuilt":
         scene = hs.upload(local, bvh="rebuilt", width=args.bvh_width, leaf_size=args.leaf_size,
-                          traversal_cost=args.traversal_cost)
+                          traversal_cost=args.traversal_cost, gpu_build=not args.host_build)
         bvh_desc = (f"rebuilt {args.bvh_width}-wide SAH, leaf<={args.leaf_size}, C_trav={args.traversal_cost:g}")
     t_scene = time.perf_counter() - t
     st = scene.stats()
     counts = hs.counts()
     setup = {"load_build_upload_s": round(t_scene, 3), "load_and_mesh_bvh_s": round(t_load, 3),
              "mesh_bvh_build": "host" if args.host_build else "gpu (crt_build_mesh_bvh)",
+             "rebuilt_bvh_build": "host" if args.host_build else "gpu (binned SAH, crt_scene_options.gpu_build)",
              "mesh_bvh_device_ms": round(hs.device_build_ms(), 2)}
     log_r(f"[scene] {args.scene}: {counts['n_indices'] // 3} triangles, {st['device_nodes']} nodes, "
           f"{st['device_bytes'] / 1e6:.1f} MB in HBM, load+build+upload {t_scene:.2f}s {setup}")

@@ -174,7 +174,9 @@ typedef struct crt_scene_options {
     float traversal_cost;     /* REBUILT: SAH cost of one node step relative to one triangle test (0 = default 2) */
     int32_t width;            /* REBUILT: 4 (default) = 4-wide nodes, stack traversal (kernel variant 4);
                                  2 = threaded binary layouts (variants 0-3) */
-    int32_t reserved[3];
+    int32_t gpu_build;        /* REBUILT: 1 = build the binned-SAH tree on the GPU (crt_scene_create_ex: the scene's
+                                 device; crt_scene_export: device 0), 0 = on the host (default) */
+    int32_t reserved[2];
 } crt_scene_options;
 
 /* ---- scene (SceneManager device half) ---- */
@@ -217,7 +219,8 @@ int  crt_renderer_set_camera(crt_renderer* r, const crt_camera_desc* cam);
  * scheduling over 4-wide nodes with a per-lane stack, 16x16-pixel workgroups; 5 = the wavefront path (trace and shade
  * kernels over a queue of active pixels); 7 = 4 with a persistent grid whose lanes take pixels from a global queue
  * (no lane waits for its wave's slowest pixel); 8 = 4 with one wave per workgroup over 8x8 tiles in cost-probe order
- * (crt_renderer_set_schedule); anything else = automatic: 8 when the render runs the cost probe (spp >= its
+ * (crt_renderer_set_schedule); 9 = 8 with K tiles per wave whose lanes take the wave's pixels in turn; anything
+ * else = automatic: 8 when the render runs the cost probe (spp >= its
  * minimum), else 7. */
 int  crt_renderer_set_kernel_variant(crt_renderer* r, int variant);
 /* Variant 5: idle lanes that trigger a queue fetch in the trace kernel (1..64, default 16) and trace/shade
@@ -230,8 +233,8 @@ long long crt_renderer_wavefront_iterations(const crt_renderer* r);   /* iterati
  * most-expensive-first (variant 7: pixels handed to lanes from a global queue; variant 8: 8x8 tiles, one wave per
  * workgroup).  Renders with fewer than min_spp samples per pixel skip the probe.  flags: CRT_SCHEDULE_XCD_BANDS
  * (variant 8: each of the 8 XCDs renders one horizontal strip of the image), CRT_SCHEDULE_FIRST_BLOCK (variant 7:
- * a wave's first 64 pixels run without refills).  Default 4, 64, 0; probe_spp 0 disables the probe.  Results never
- * depend on the order. */
+ * a wave's first 64 pixels run without refills), and in bits 8-15 the tiles per wave of variant 9 (default 2).
+ * Default 4, 64, 0; probe_spp 0 disables the probe.  Results never depend on the order. */
 #define CRT_SCHEDULE_XCD_BANDS  1
 #define CRT_SCHEDULE_FIRST_BLOCK 2
 int  crt_renderer_set_schedule(crt_renderer* r, int probe_spp, int min_spp, int flags);

@@ -109,14 +109,14 @@ class HostScene:
         return idx, fm
 
     def upload(self, device: int = 0, bvh: str = "reference", leaf_size: int = 0, layouts: int = 0,
-               traversal_cost: float = 0.0, width: int = 0) -> "Scene":
+               traversal_cost: float = 0.0, width: int = 0, gpu_build: bool = False) -> "Scene":
         """Device scene.  bvh="reference": the reference's BVHs, bit-exact (crth_scene_upload);
         bvh="rebuilt": binned-SAH BVH with the reference's hit rule (crt_scene_create_ex)."""
         h = C.c_void_p()
-        if bvh == "reference" and not leaf_size and not layouts and not traversal_cost and not width:
+        if bvh == "reference" and not leaf_size and not layouts and not traversal_cost and not width and not gpu_build:
             check_host(_lib.host().crth_scene_upload(self.h, int(device), C.byref(h)), "crth_scene_upload")
             return Scene(h, device)
-        o = scene_options(bvh, leaf_size, layouts, traversal_cost, width)
+        o = scene_options(bvh, leaf_size, layouts, traversal_cost, width, gpu_build)
         d = self.desc()
         check(_lib.hip().crt_scene_create_ex(C.byref(d), int(device), C.byref(o), C.byref(h)), "crt_scene_create_ex")
         return Scene(h, device)
@@ -140,7 +140,7 @@ class HostScene:
 
 
 def scene_options(bvh: str = "reference", leaf_size: int = 0, layouts: int = 0, traversal_cost: float = 0.0,
-                  width: int = 0):
+                  width: int = 0, gpu_build: bool = False):
     modes = {"reference": _lib.BVH_REFERENCE, "rebuilt": _lib.BVH_REBUILT}
     if bvh not in modes:
         raise ValueError(f"bvh must be one of {sorted(modes)}")
@@ -148,6 +148,7 @@ def scene_options(bvh: str = "reference", leaf_size: int = 0, layouts: int = 0, 
     o.bvh, o.leaf_size, o.layouts = modes[bvh], int(leaf_size), int(layouts)
     o.traversal_cost = float(traversal_cost)
     o.width = int(width)
+    o.gpu_build = int(bool(gpu_build))
     return o
 
 
@@ -211,8 +212,9 @@ class Renderer:
     def init_rand(self, seed: int = 41, subsequence_base: int = 0, stream=None):
         check(_lib.hip().crt_renderer_init_rand(self.h, int(seed), int(subsequence_base), stream), "init_rand")
 
-    def set_schedule(self, probe_spp: int = 4, min_spp: int = 64, xcd_bands: bool = False, first_block: bool = False):
-        flags = (1 if xcd_bands else 0) | (2 if first_block else 0)
+    def set_schedule(self, probe_spp: int = 4, min_spp: int = 64, xcd_bands: bool = False, first_block: bool = False,
+                     tiles_per_wave: int = 2):
+        flags = (1 if xcd_bands else 0) | (2 if first_block else 0) | ((int(tiles_per_wave) & 0xff) << 8)
         check(_lib.hip().crt_renderer_set_schedule(self.h, int(probe_spp), int(min_spp), flags), "set_schedule")
 
     def set_kernel_variant(self, variant: int):

@@ -71,7 +71,8 @@ class SceneStats(C.Structure):
 
 class SceneOptions(C.Structure):
     _fields_ = [("bvh", C.c_int32), ("leaf_size", C.c_int32), ("layouts", C.c_int32),
-                ("traversal_cost", C.c_float), ("width", C.c_int32), ("reserved", C.c_int32 * 3)]
+                ("traversal_cost", C.c_float), ("width", C.c_int32), ("gpu_build", C.c_int32),
+                ("reserved", C.c_int32 * 2)]
 
 
 BVH_REFERENCE = 0

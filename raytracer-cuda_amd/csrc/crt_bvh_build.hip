@@ -703,3 +703,373 @@ extern "C" int crt_build_mesh_bvh(int device, const float* positions, uint32_t v
     if (build_ms) BTRY(hipEventElapsedTime(build_ms, e0, e1));
     return CRT_OK;
 }
+
+// ======================================================================================================
+// The CRT_BVH_REBUILT binned-SAH build (crt_sah.h's Builder) on the GPU, level by level.
+//
+// Same rules as the host builder: node box = padded (pad_box) bounds of its items; 32 bins per axis over
+// the centroid extent; SAH sweep with traversal cost C_trav and unit primitive cost; leaf when the node
+// may be a leaf (no spheres, count <= leaf_size) and splitting does not pay; count 1 is a leaf; no usable
+// split (all centroids equal) splits in half.  Bin counts and boxes are order-independent, so the splits
+// equal the host's; the partition here is stable (the host's std::partition is not), so only the order
+// of items inside a node can differ — any order is a valid tree for the rank rule.
+// ======================================================================================================
+#include "crt_sah.h"
+
+namespace {
+
+constexpr int SAH_BINS = 32;
+constexpr int SAH_RED = 13 + 3 * SAH_BINS * 7;   // box lo3 hi3, centroid lo3 hi3, spheres; bins: count lo3 hi3
+
+struct SahLevel {
+    int* start;     // per tmp node
+    int* count;
+    int* left;      // tmp id of the left child, -1 = leaf
+    float* lo;      // padded box, 3 per node
+    float* hi;
+    int* axis;      // split axis, -1 = split in half
+    int* split;     // first bin of the right side
+    int* nless;
+    float* clo;     // centroid lower bound (3 per node)
+    float* scale;   // bins / extent per axis, 0 = axis not binned
+    int* internal;  // level-local: 1 when the node splits
+};
+
+__device__ __forceinline__ void pad_box_dev(float lo[3], float hi[3]) {   // crt_sah::pad_box
+    float m = 1.0f;
+    for (int a = 0; a < 3; ++a) m = fmaxf(m, fmaxf(fabsf(lo[a]), fabsf(hi[a])));
+    const float pad = 1e-5f * m;
+    for (int a = 0; a < 3; ++a) { lo[a] -= pad; hi[a] += pad; }
+}
+__device__ __forceinline__ float half_area_dev(const float lo[3], const float hi[3]) {
+    const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return dx * dy + dy * dz + dz * dx;
+}
+
+__global__ void k_sah_reset(uint32_t* __restrict__ red, int n_lev) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)n_lev * SAH_RED) return;
+    const int w = (int)(i % SAH_RED);
+    uint32_t v;
+    if (w < 12) v = (w % 6) < 3 ? ord(INFINITY) : ord(-INFINITY);     // lo3 hi3, clo3 chi3
+    else if (w == 12) v = 0u;
+    else {
+        const int k = (w - 13) % 7;
+        v = k == 0 ? 0u : k < 4 ? ord(INFINITY) : ord(-INFINITY);
+    }
+    red[i] = v;
+}
+
+// node bounds: item boxes, centroid bounds, sphere count
+__global__ void k_sah_bounds(const int* __restrict__ seg, const uint32_t* __restrict__ perm, const float* __restrict__ ilo,
+                             const float* __restrict__ ihi, const float* __restrict__ ic, const int* __restrict__ isph,
+                             int n, uint32_t* __restrict__ red) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const LaneSeg L = lane_seg(seg, p, n);
+    if (L.s0 < 0) return;
+    const bool act = L.s >= 0;
+    const uint32_t t = act ? perm[p] : 0;
+    uint32_t v[12];
+    for (int a = 0; a < 3; ++a) {
+        v[a] = act ? ord(ilo[(size_t)a * n + t]) : 0xffffffffu;
+        v[3 + a] = act ? ord(ihi[(size_t)a * n + t]) : 0u;
+        v[6 + a] = act ? ord(ic[(size_t)a * n + t]) : 0xffffffffu;
+        v[9 + a] = act ? ord(ic[(size_t)a * n + t]) : 0u;
+    }
+    const uint32_t sp = act ? (uint32_t)isph[t] : 0u;
+    if (L.uniform) {
+        uint32_t r[12];
+        for (int k = 0; k < 12; ++k) r[k] = ((k % 6) < 3) ? wave_min(v[k]) : wave_max(v[k]);
+        const uint64_t nsp = __ballot(sp != 0);
+        if ((threadIdx.x & 63) == 0) {
+            uint32_t* o = red + (size_t)L.s0 * SAH_RED;
+            for (int k = 0; k < 12; ++k) ((k % 6) < 3) ? atomicMin(&o[k], r[k]) : atomicMax(&o[k], r[k]);
+            if (nsp) atomicAdd(&o[12], (uint32_t)__popcll(nsp));
+        }
+    } else if (act) {
+        uint32_t* o = red + (size_t)L.s * SAH_RED;
+        for (int k = 0; k < 12; ++k) ((k % 6) < 3) ? atomicMin(&o[k], v[k]) : atomicMax(&o[k], v[k]);
+        if (sp) atomicAdd(&o[12], 1u);
+    }
+}
+
+// per node: padded box, bin parameters (crt_sah.h build_range)
+__global__ void k_sah_prep(SahLevel N, int base, int n_lev, const uint32_t* __restrict__ red) {
+    const int li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= n_lev) return;
+    const int X = base + li;
+    const uint32_t* r = red + (size_t)li * SAH_RED;
+    float lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) { lo[a] = unord(r[a]); hi[a] = unord(r[3 + a]); }
+    pad_box_dev(lo, hi);
+    for (int a = 0; a < 3; ++a) {
+        N.lo[3 * (size_t)X + a] = lo[a];
+        N.hi[3 * (size_t)X + a] = hi[a];
+        const float clo = unord(r[6 + a]), chi = unord(r[9 + a]);
+        const float ext = chi - clo;
+        N.clo[3 * (size_t)X + a] = clo;
+        N.scale[3 * (size_t)X + a] = (ext > 0.f && N.count[X] > 1) ? (float)SAH_BINS / ext : 0.f;
+    }
+}
+
+__device__ __forceinline__ int sah_bin(float c, float clo, float scale) {
+    return min(SAH_BINS - 1, (int)((c - clo) * scale));
+}
+
+__global__ void k_sah_bins(const int* __restrict__ seg, const uint32_t* __restrict__ perm, const float* __restrict__ ilo,
+                           const float* __restrict__ ihi, const float* __restrict__ ic, int n, SahLevel N, int base,
+                           uint32_t* __restrict__ red) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int s = seg[p];
+    if (s < 0) return;
+    const int X = base + s;
+    const uint32_t t = perm[p];
+    uint32_t lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) { lo[k] = ord(ilo[(size_t)k * n + t]); hi[k] = ord(ihi[(size_t)k * n + t]); }
+    for (int a = 0; a < 3; ++a) {
+        const float sc = N.scale[3 * (size_t)X + a];
+        if (sc == 0.f) continue;
+        const int b = sah_bin(ic[(size_t)a * n + t], N.clo[3 * (size_t)X + a], sc);
+        uint32_t* o = red + (size_t)s * SAH_RED + 13 + (a * SAH_BINS + b) * 7;
+        atomicAdd(&o[0], 1u);
+        for (int k = 0; k < 3; ++k) { atomicMin(&o[1 + k], lo[k]); atomicMax(&o[4 + k], hi[k]); }
+    }
+}
+
+// SAH sweep and leaf test (crt_sah.h build_range, same float expressions)
+__global__ void k_sah_decide(SahLevel N, int base, int n_lev, const uint32_t* __restrict__ red, int leaf_size,
+                             float trav_cost) {
+    const int li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= n_lev) return;
+    const int X = base + li;
+    const uint32_t* r = red + (size_t)li * SAH_RED;
+    const int count = N.count[X];
+    N.internal[li] = 0;
+    N.left[X] = -1;
+    if (count <= 1) return;
+    const bool leaf_ok = r[12] == 0 && count <= leaf_size;
+    float best_cost = INFINITY;
+    int best_axis = -1, best_split = 0;
+    for (int a = 0; a < 3; ++a) {
+        if (N.scale[3 * (size_t)X + a] == 0.f) continue;
+        const uint32_t* bins = r + 13 + a * SAH_BINS * 7;
+        float right_area[SAH_BINS];
+        int right_cnt[SAH_BINS];
+        float rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int rc = 0;
+        for (int b = SAH_BINS - 1; b > 0; --b) {
+            const uint32_t* o = bins + b * 7;
+            rc += (int)o[0];
+            for (int q = 0; q < 3; ++q) { rlo[q] = fminf(rlo[q], unord(o[1 + q])); rhi[q] = fmaxf(rhi[q], unord(o[4 + q])); }
+            right_cnt[b] = rc;
+            right_area[b] = rc ? half_area_dev(rlo, rhi) : 0.f;
+        }
+        float llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int lc = 0;
+        for (int b = 0; b < SAH_BINS - 1; ++b) {
+            const uint32_t* o = bins + b * 7;
+            lc += (int)o[0];
+            for (int q = 0; q < 3; ++q) { llo[q] = fminf(llo[q], unord(o[1 + q])); lhi[q] = fmaxf(lhi[q], unord(o[4 + q])); }
+            if (lc == 0 || right_cnt[b + 1] == 0) continue;
+            const float cost = half_area_dev(llo, lhi) * lc + right_area[b + 1] * right_cnt[b + 1];
+            if (cost < best_cost) { best_cost = cost; best_axis = a; best_split = b + 1; }
+        }
+    }
+    const float node_area = fmaxf(half_area_dev(&N.lo[3 * (size_t)X], &N.hi[3 * (size_t)X]), 1e-30f);
+    if (leaf_ok && (best_axis < 0 || trav_cost + best_cost / node_area >= (float)count)) return;
+    N.axis[X] = best_axis;
+    N.split[X] = best_split;
+    int l = count / 2;                            // no usable split: halves (every centroid is the same)
+    if (best_axis >= 0) {
+        l = 0;
+        const uint32_t* bins = r + 13 + best_axis * SAH_BINS * 7;
+        for (int b = 0; b < best_split; ++b) l += (int)bins[b * 7];
+    }
+    N.nless[X] = l;
+    N.internal[li] = 1;
+}
+
+// ranks of the level's splitting nodes (single workgroup); stats[0] = how many
+__global__ __launch_bounds__(1024) void k_sah_scan(SahLevel N, int n_lev, int* __restrict__ irank, int* __restrict__ stats) {
+    __shared__ int part[1024];
+    const int tid = threadIdx.x, per = (n_lev + 1023) / 1024;
+    const int b = min(n_lev, tid * per), e = min(n_lev, b + per);
+    int c = 0;
+    for (int i = b; i < e; ++i) c += N.internal[i];
+    part[tid] = c;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int add = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += add;
+        __syncthreads();
+    }
+    int r = part[tid] - c;
+    for (int i = b; i < e; ++i) irank[i] = N.internal[i] ? r++ : -1;
+    if (tid == 1023) stats[0] = part[1023];
+}
+
+__global__ void k_sah_children(SahLevel N, int base, int n_lev, const int* __restrict__ irank, int next_base) {
+    const int li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= n_lev || irank[li] < 0) return;
+    const int X = base + li, cl = next_base + 2 * irank[li], l = N.nless[X];
+    N.left[X] = cl;
+    N.start[cl] = N.start[X];
+    N.count[cl] = l;
+    N.start[cl + 1] = N.start[X] + l;
+    N.count[cl + 1] = N.count[X] - l;
+    N.left[cl] = N.left[cl + 1] = -1;
+}
+
+__global__ void k_sah_flags(const int* __restrict__ seg, const uint32_t* __restrict__ perm, const float* __restrict__ ic,
+                            int n, SahLevel N, int base, uint32_t* __restrict__ flags) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int s = seg[p];
+    uint32_t f = 0;
+    if (s >= 0 && N.left[base + s] >= 0) {
+        const int X = base + s, a = N.axis[X];
+        if (a >= 0) f = sah_bin(ic[(size_t)a * n + perm[p]], N.clo[3 * (size_t)X + a], N.scale[3 * (size_t)X + a]) < N.split[X];
+        else f = (p - N.start[X]) < N.nless[X];
+    }
+    flags[p] = f;
+}
+
+// stable two-sided partition; every position of a splitting node moves to its child's range
+__global__ void k_sah_scatter(const int* __restrict__ seg, const uint32_t* __restrict__ flags,
+                              const uint32_t* __restrict__ lb, const uint32_t* __restrict__ perm,
+                              uint32_t* __restrict__ perm2, int* __restrict__ seg2, int n, SahLevel N, int base,
+                              int next_base) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int s = seg[p];
+    if (s < 0 || N.left[base + s] < 0) { perm2[p] = perm[p]; seg2[p] = -1; return; }
+    const int X = base + s, st = N.start[X], l = N.nless[X];
+    const int less = (int)(lb[p] - lb[st]);
+    const int dst = flags[p] ? st + less : st + l + ((p - st) - less);
+    perm2[dst] = perm[p];
+    const int c = N.left[X] + (dst - st < l ? 0 : 1);
+    seg2[dst] = c - next_base;
+}
+
+}  // namespace
+
+// Host entry used by crt_scene_create_ex / crt_scene_export (gpu_build): the tree crt_sah::Builder would build,
+// as Builder::nodes() (root 0) and the item order (indices into `items`).
+int crtx_build_sah_gpu(int device, const std::vector<crt_sah::Item>& items, int leaf_size, float trav_cost,
+                       std::vector<crt_sah::Node>* nodes_out, std::vector<int>* order_out, int* max_depth) {
+    const int n = (int)items.size();
+    if (n <= 0) return crtx_set_error(CRT_ERR_INVALID_ARGUMENT, "SAH build: no items");
+    int ndev = 0;
+    BTRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return crtx_set_error(CRT_ERR_INVALID_ARGUMENT, "device ordinal out of range");
+    BTRY(hipSetDevice(device));
+    DeviceArena A;
+    hipStream_t st = nullptr;
+    std::vector<float> h(9 * (size_t)n);
+    std::vector<int> hs((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        for (int a = 0; a < 3; ++a) {
+            h[(size_t)a * n + i] = items[i].lo[a];
+            h[3 * (size_t)n + (size_t)a * n + i] = items[i].hi[a];
+            h[6 * (size_t)n + (size_t)a * n + i] = items[i].c[a];
+        }
+        hs[i] = items[i].sphere ? 1 : 0;
+    }
+    float* d_item = nullptr;
+    int* d_sph = nullptr;
+    BTRY(A.alloc(&d_item, 9 * (size_t)n));
+    BTRY(A.alloc(&d_sph, n));
+    BTRY(hipMemcpyAsync(d_item, h.data(), h.size() * 4, hipMemcpyHostToDevice, st));
+    BTRY(hipMemcpyAsync(d_sph, hs.data(), hs.size() * 4, hipMemcpyHostToDevice, st));
+    const float *d_lo = d_item, *d_hi = d_item + 3 * (size_t)n, *d_c = d_item + 6 * (size_t)n;
+    const size_t cap = 2 * (size_t)n + 2;
+    const size_t lev_cap = (size_t)n + 2;
+    const int nb = (n + SCAN_ITEMS - 1) / SCAN_ITEMS;
+    uint32_t *d_perm, *d_perm2, *d_flags, *d_lb, *d_bsum, *d_red;
+    int *d_seg, *d_seg2, *d_irank, *d_stats;
+    BTRY(A.alloc(&d_perm, n));
+    BTRY(A.alloc(&d_perm2, n));
+    BTRY(A.alloc(&d_flags, n));
+    BTRY(A.alloc(&d_lb, n));
+    BTRY(A.alloc(&d_bsum, nb));
+    BTRY(A.alloc(&d_seg, n));
+    BTRY(A.alloc(&d_seg2, n));
+    BTRY(A.alloc(&d_irank, lev_cap));
+    BTRY(A.alloc(&d_stats, 2));
+    SahLevel N;
+    BTRY(A.alloc(&N.start, cap));
+    BTRY(A.alloc(&N.count, cap));
+    BTRY(A.alloc(&N.left, cap));
+    BTRY(A.alloc(&N.lo, 3 * cap));
+    BTRY(A.alloc(&N.hi, 3 * cap));
+    BTRY(A.alloc(&N.axis, cap));
+    BTRY(A.alloc(&N.split, cap));
+    BTRY(A.alloc(&N.nless, cap));
+    BTRY(A.alloc(&N.clo, 3 * cap));
+    BTRY(A.alloc(&N.scale, 3 * cap));
+    BTRY(A.alloc(&N.internal, lev_cap));
+    size_t red_cap = 0;
+    d_red = nullptr;
+    hipLaunchKernelGGL(k_iota, dim3(blocks(n)), dim3(256), 0, st, d_perm, d_seg, n);
+    {
+        const int zero = 0;
+        BTRY(hipMemcpyAsync(N.start, &zero, 4, hipMemcpyHostToDevice, st));
+        BTRY(hipMemcpyAsync(N.count, &n, 4, hipMemcpyHostToDevice, st));
+        BTRY(hipMemsetAsync(N.left, 0xff, 4, st));
+    }
+    std::vector<int> level_off = {0, 1};
+    for (;;) {
+        const int base = level_off[level_off.size() - 2], n_lev = level_off.back() - base;
+        if ((size_t)n_lev * SAH_RED > red_cap) {   // grow the per-level reduction area
+            red_cap = std::max((size_t)n_lev * SAH_RED, 2 * red_cap);
+            BTRY(A.alloc(&d_red, red_cap));
+        }
+        hipLaunchKernelGGL(k_sah_reset, dim3(blocks((size_t)n_lev * SAH_RED)), dim3(256), 0, st, d_red, n_lev);
+        hipLaunchKernelGGL(k_sah_bounds, dim3(blocks(n)), dim3(256), 0, st, d_seg, d_perm, d_lo, d_hi, d_c, d_sph, n, d_red);
+        hipLaunchKernelGGL(k_sah_prep, dim3(blocks(n_lev)), dim3(256), 0, st, N, base, n_lev, d_red);
+        hipLaunchKernelGGL(k_sah_bins, dim3(blocks(n)), dim3(256), 0, st, d_seg, d_perm, d_lo, d_hi, d_c, n, N, base, d_red);
+        hipLaunchKernelGGL(k_sah_decide, dim3(blocks(n_lev)), dim3(256), 0, st, N, base, n_lev, d_red, leaf_size, trav_cost);
+        hipLaunchKernelGGL(k_sah_scan, dim3(1), dim3(1024), 0, st, N, n_lev, d_irank, d_stats);
+        int n_int = 0;
+        BTRY(hipMemcpyAsync(&n_int, d_stats, 4, hipMemcpyDeviceToHost, st));
+        BTRY(hipStreamSynchronize(st));
+        if (n_int == 0) break;
+        const int next_base = level_off.back();
+        if ((size_t)next_base + 2 * (size_t)n_int > cap) return crtx_set_error(CRT_ERR_HIP, "SAH build: node table overflow");
+        hipLaunchKernelGGL(k_sah_children, dim3(blocks(n_lev)), dim3(256), 0, st, N, base, n_lev, d_irank, next_base);
+        hipLaunchKernelGGL(k_sah_flags, dim3(blocks(n)), dim3(256), 0, st, d_seg, d_perm, d_c, n, N, base, d_flags);
+        hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(256), 0, st, d_flags, d_lb, d_bsum, n);
+        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, st, d_bsum, nb);
+        hipLaunchKernelGGL(k_scan_add, dim3(blocks(n)), dim3(256), 0, st, d_lb, d_bsum, n);
+        hipLaunchKernelGGL(k_sah_scatter, dim3(blocks(n)), dim3(256), 0, st, d_seg, d_flags, d_lb, d_perm, d_perm2, d_seg2,
+                           n, N, base, next_base);
+        std::swap(d_perm, d_perm2);
+        std::swap(d_seg, d_seg2);
+        level_off.push_back(next_base + 2 * n_int);
+    }
+    BTRY(hipGetLastError());
+    const int total = level_off.back();
+    std::vector<int> hstart(total), hcount(total), hleft(total);
+    std::vector<float> hlo(3 * (size_t)total), hhi(3 * (size_t)total);
+    std::vector<uint32_t> hperm(n);
+    BTRY(hipMemcpy(hstart.data(), N.start, (size_t)total * 4, hipMemcpyDeviceToHost));
+    BTRY(hipMemcpy(hcount.data(), N.count, (size_t)total * 4, hipMemcpyDeviceToHost));
+    BTRY(hipMemcpy(hleft.data(), N.left, (size_t)total * 4, hipMemcpyDeviceToHost));
+    BTRY(hipMemcpy(hlo.data(), N.lo, (size_t)total * 12, hipMemcpyDeviceToHost));
+    BTRY(hipMemcpy(hhi.data(), N.hi, (size_t)total * 12, hipMemcpyDeviceToHost));
+    BTRY(hipMemcpy(hperm.data(), d_perm, (size_t)n * 4, hipMemcpyDeviceToHost));
+    nodes_out->assign((size_t)total, crt_sah::Node{});
+    for (int t = 0; t < total; ++t) {
+        crt_sah::Node& o = (*nodes_out)[t];
+        for (int a = 0; a < 3; ++a) { o.lo[a] = hlo[3 * (size_t)t + a]; o.hi[a] = hhi[3 * (size_t)t + a]; }
+        o.child[0] = hleft[t];
+        o.child[1] = hleft[t] < 0 ? -1 : hleft[t] + 1;
+        o.first = hstart[t];
+        o.count = hleft[t] < 0 ? hcount[t] : 0;
+    }
+    order_out->assign(hperm.begin(), hperm.end());
+    if (max_depth) *max_depth = (int)level_off.size() - 2;
+    return CRT_OK;
+}

@@ -31,6 +31,8 @@ static int set_error(int code, const std::string& msg) {
     return code;
 }
 int crtx_set_error(int code, const std::string& msg) { return set_error(code, msg); }   // crt_bvh_build.hip
+int crtx_build_sah_gpu(int device, const std::vector<crt_sah::Item>& items, int leaf_size, float trav_cost,
+                       std::vector<crt_sah::Node>* nodes_out, std::vector<int>* order_out, int* max_depth);
 #define HIP_TRY(expr)                                                                           \
     do {                                                                                        \
         hipError_t e_ = (expr);                                                                 \
@@ -71,6 +73,7 @@ struct RenderParams {
     int n_slots;
     int tiles_x;                          // variant 8: 8x8 tiles per row (order[] holds tile indices)
     int first_block_exclusive;            // variant 7: a wave refills lanes only after its first 64 pixels are done
+    int tiles_per_wave;                   // variant 9: 8x8 tiles in a wave's local pixel list
     uint32_t* __restrict__ probe_cost;    // probe launch (variant 4): rays per pixel; nothing else is written
 };
 
@@ -967,7 +970,7 @@ __device__ unsigned long long g_wave_prof[2 * 4 * 65536];
 
 // Waves per workgroup: 4 (16x16 pixels), or 1 for variant 8 (one 8x8 tile per workgroup, so a finished wave frees
 // its slot at once instead of holding it until its three siblings end).
-template <int VARIANT> struct KernelShape { static constexpr int waves = VARIANT == 8 ? 1 : 4; };
+template <int VARIANT> struct KernelShape { static constexpr int waves = (VARIANT == 8 || VARIANT == 9) ? 1 : 4; };
 
 template <bool COUNT, int VARIANT, int MINW>
 __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_render_kernel(RenderParams P) {
@@ -977,7 +980,11 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     constexpr int WGW = KernelShape<VARIANT>::waves;
     __shared__ WaveLds lds[VARIANT >= 1 ? WGW : 1];
     // variant 4: 16 LDS stack entries per lane at 5 waves/SIMD; 12 at 6+ so 6 workgroups fit the 160 KiB
-    constexpr bool PERSIST = VARIANT == 7;
+    // variant 9: variant 7's lane refill from a wave-local list instead of the global queue: workgroup b (one wave)
+    // owns tiles order[b*K .. b*K+K-1] (K = P.tiles_per_wave, tiles most expensive first) and its lanes take their
+    // pixels in turn
+    constexpr bool LOCALQ = VARIANT == 9;
+    constexpr bool PERSIST = VARIANT == 7 || LOCALQ;
     constexpr bool TILED = VARIANT == 8;    // variant 4 with one wave per workgroup and a tile order
     constexpr bool WIDE = VARIANT == 4 || PERSIST || TILED;
     constexpr int SD = WIDE ? (MINW >= 7 ? 11 : MINW >= 6 ? 12 : STACK_LDS) : 1;
@@ -1045,7 +1052,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         uint32_t* stk = stack_lds + wave * SD * 64;
         const float INF = __builtin_inff();
         const size_t n_pix = (size_t)P.width * P.height;
-        const uint32_t total_slots = (uint32_t)P.n_slots;
+        const uint32_t total_slots = LOCALQ ? (blockIdx.x + 1u) * (uint32_t)P.tiles_per_wave * 64u : (uint32_t)P.n_slots;
+        uint32_t next_block = blockIdx.x * (uint32_t)P.tiles_per_wave * 64u;   // LOCALQ: the wave's next tile
         const uint64_t below = (1ull << lane) - 1ull;
         bool live = false, has_result = false, have = false;
         int node = -1, sp = 0, hit = -1, px = 0, py = 0, ppix = 0;
@@ -1082,16 +1090,30 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     const uint64_t need = __ballot(!have);
                     if (need == 0) break;
                     if (used >= 64u) {
-                        uint32_t b = 0;
-                        if (lane == 0) b = atomicAdd(P.queue, 64u);
-                        pool = __builtin_amdgcn_readfirstlane(b);
+                        if (LOCALQ) {
+                            pool = next_block;
+                            next_block += 64u;
+                        } else {
+                            uint32_t b = 0;
+                            if (lane == 0) b = atomicAdd(P.queue, 64u);
+                            pool = __builtin_amdgcn_readfirstlane(b);
+                        }
                         used = 0;
                         if (pool >= total_slots) { exhausted = true; break; }
                     }
                     const uint32_t take = min((uint32_t)__popcll(need), 64u - used);
                     const uint32_t rank = (uint32_t)__popcll(need & below);
                     if (!have && rank < take && pool + used + rank < total_slots) {
-                        const uint32_t pixel = P.order[pool + used + rank];
+                        uint32_t pixel;
+                        if (LOCALQ) {                 // slot -> (tile order[slot / 64], pixel slot % 64 of it)
+                            const uint32_t slot = pool + used + rank, tile = P.order[slot >> 6], q = slot & 63u;
+                            const int tx = (int)(tile % (uint32_t)P.tiles_x) * 8 + (int)(q & 7u);
+                            const int ty = (int)(tile / (uint32_t)P.tiles_x) * 8 + (int)(q >> 3);
+                            pixel = (tile != 0xffffffffu && tx < P.width && ty < P.height) ? (uint32_t)(ty * P.width + tx)
+                                                                                          : 0xffffffffu;
+                        } else {
+                            pixel = P.order[pool + used + rank];
+                        }
                         if (pixel != 0xffffffffu) {
                             ppix = (int)pixel;
                             px = ppix % P.width;
@@ -1794,6 +1816,11 @@ __global__ void crt_order_bands_kernel(const uint32_t* __restrict__ sorted, int 
     order[b] = (j < per && t < n_tiles) ? (sorted ? sorted[t] : (uint32_t)t) : 0xffffffffu;
 }
 
+__global__ void crt_order_iota_kernel(uint32_t* __restrict__ order, int n) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) order[t] = (uint32_t)t;
+}
+
 // No probe: 8x8 tiles in row order, pixels row-major inside a tile (a wave's first 64 slots are one tile, so
 // its primary rays are coherent); slots of partial edge tiles hold ~0.
 __global__ void crt_order_tiles_kernel(uint32_t* __restrict__ order, int width, int height, int n_slots) {
@@ -2007,7 +2034,8 @@ struct Rebuilt {
     std::vector<float4> chain;                 // their reference scene-level leaf boxes (2 float4 per box)
     static constexpr int kMaxRaySpheres = 8;
 
-    bool build(const Flattener& F, int leaf_size, int layouts, float trav_cost, int wide) {
+    // gpu_device >= 0: the binned-SAH tree is built on that GPU (crtx_build_sah_gpu, crt_bvh_build.hip)
+    bool build(const Flattener& F, int leaf_size, int layouts, float trav_cost, int wide, int gpu_device = -1) {
         width = wide;
         const int n = (int)(F.prims.size() / 3);
         std::vector<crt_sah::Item> items;
@@ -2082,12 +2110,25 @@ struct Rebuilt {
             }
             return true;
         }
-        crt_sah::Builder B(std::move(items), leaf_size, trav_cost);
-        B.build();
-        max_depth = B.max_depth();
-        const auto& its = B.items();
+        std::vector<crt_sah::Node> bnv;
+        std::vector<crt_sah::Item> its;
+        if (gpu_device >= 0) {
+            std::vector<int> order;
+            if (crtx_build_sah_gpu(gpu_device, items, leaf_size, trav_cost, &bnv, &order, &max_depth) != CRT_OK) {
+                err = std::string("GPU SAH build: ") + crt_last_error();
+                return false;
+            }
+            its.resize(order.size());
+            for (size_t i = 0; i < order.size(); ++i) its[i] = items[order[i]];
+        } else {
+            crt_sah::Builder B(std::move(items), leaf_size, trav_cost);
+            B.build();
+            max_depth = B.max_depth();
+            bnv = B.nodes();
+            its = B.items();
+        }
         if (width == 4) {
-            if (!emit4(F, B.nodes(), its)) return false;
+            if (!emit4(F, bnv, its)) return false;
             append_ray_spheres();
             return true;
         }
@@ -2097,7 +2138,7 @@ struct Rebuilt {
             for (int q = 0; q < 3; ++q) prims[3 * i + q] = F.prims[3 * p + q];
             rank_code[F.rank_of[p]] = its[i].sphere ? (SPHERE_BIT | (int)i) : (int)i;
         }
-        const auto& bn = B.nodes();
+        const auto& bn = bnv;
         n_nodes = (int)bn.size();
         nodes.reserve(2 * (size_t)n_nodes * layouts);
         for (int l = 0; l < layouts; ++l) {
@@ -2232,6 +2273,7 @@ struct crt_renderer {
     int probe_min_spp = 64;        // renders with fewer samples per pixel skip the probe
     int xcd_bands = 0;             // variant 8: each XCD renders one horizontal strip (see crt_order_bands_kernel)
     int first_block_exclusive = 0; // variant 7: see RenderParams::first_block_exclusive
+    int tiles_per_wave = 2;        // variant 9
     uint32_t* d_sorted = nullptr;  // variant 8: tiles sorted per band
     int n_cus = 0;
     int variant = 3;               // see crt_renderer_set_kernel_variant
@@ -2289,7 +2331,7 @@ int crt_scene_create(const crt_scene_desc* D, int device, crt_scene** out) {
 // Host half of scene creation: flatten the reference BVHs (ranks, reachability) and, for CRT_BVH_REBUILT,
 // build the SAH tree.  Shared by crt_scene_create_ex and crt_scene_export.
 static int build_scene_arrays(const crt_scene_desc* D, const crt_scene_options* opts, crt_scene_options& o,
-                              Flattener& F, Rebuilt& RB) {
+                              Flattener& F, Rebuilt& RB, int gpu_device) {
     o = crt_scene_options{};
     if (opts) o = *opts;
     if (o.bvh != CRT_BVH_REFERENCE && o.bvh != CRT_BVH_REBUILT) return set_error(CRT_ERR_INVALID_ARGUMENT, "unknown bvh mode");
@@ -2307,7 +2349,8 @@ static int build_scene_arrays(const crt_scene_desc* D, const crt_scene_options* 
     F.finalize_ranks();
     if (o.bvh == CRT_BVH_REBUILT) {
         if (o.width == 4) o.layouts = 1;
-        if (!RB.build(F, o.leaf_size, o.layouts, o.traversal_cost, o.width)) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene: " + RB.err);
+        if (!RB.build(F, o.leaf_size, o.layouts, o.traversal_cost, o.width, o.gpu_build ? gpu_device : -1))
+            return set_error(CRT_ERR_INVALID_ARGUMENT, "scene: " + RB.err);
         if ((size_t)RB.n_nodes * o.layouts * (o.width == 4 ? 8 : 2) >= (size_t)1 << 31)
             return set_error(CRT_ERR_INVALID_ARGUMENT, "scene too large");
     }
@@ -2322,7 +2365,7 @@ int crt_scene_export(const crt_scene_desc* D, const crt_scene_options* opts, flo
     crt_scene_options o;
     Flattener F{D};
     Rebuilt RB;
-    if (int rc = build_scene_arrays(D, opts, o, F, RB)) return rc;
+    if (int rc = build_scene_arrays(D, opts, o, F, RB, 0)) return rc;
     const bool rebuilt = o.bvh == CRT_BVH_REBUILT;
     const std::vector<float4>& N = rebuilt ? RB.nodes : F.nodes;
     const std::vector<float4>& Pr = rebuilt ? RB.prims : F.prims;
@@ -2394,7 +2437,7 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
     crt_scene_options o;
     Flattener F{D};
     Rebuilt RB;
-    if (int rc = build_scene_arrays(D, opts, o, F, RB)) return rc;
+    if (int rc = build_scene_arrays(D, opts, o, F, RB, device)) return rc;
     const bool rebuilt = o.bvh == CRT_BVH_REBUILT;
     std::vector<float4> mats;
     for (int i = 0; i < D->n_materials; ++i) {
@@ -2564,7 +2607,7 @@ int crt_renderer_init_rand(crt_renderer* R, unsigned long long seed, unsigned lo
 }
 
 int crt_renderer_set_kernel_variant(crt_renderer* R, int variant) {
-    if (!R || variant < 0 || variant > 8 || variant == 6) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant");
+    if (!R || variant < 0 || variant > 9 || variant == 6) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant");
     R->variant = variant;
     return CRT_OK;
 }
@@ -2575,6 +2618,7 @@ int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int f
     R->probe_min_spp = min_spp;
     R->xcd_bands = (flags & 1) ? 1 : 0;
     R->first_block_exclusive = (flags & 2) ? 1 : 0;
+    R->tiles_per_wave = ((flags >> 8) & 0xff) ? ((flags >> 8) & 0xff) : 2;
     return CRT_OK;
 }
 
@@ -2698,7 +2742,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.accumulate = (flags & CRT_RENDER_ACCUMULATE) ? 1 : 0;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     P.ovf = nullptr;
-    P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0;
+    P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0; P.tiles_per_wave = 1;
     P.stack_cap = S->stack_cap;
     P.sphere_first = S->sphere_first;
     P.n_ray_spheres = S->n_ray_spheres;
@@ -2755,9 +2799,9 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     // 8 (probe-ordered tiles, one wave per workgroup) when the render runs the cost probe, 7 (lanes refill from a
     // pixel queue) for short renders such as the 1-spp interactive frames
     int wv = R->variant;
-    if (S->width == 4 && wv != 4 && wv != 5 && wv != 7 && wv != 8)
+    if (S->width == 4 && wv != 4 && wv != 5 && wv != 7 && wv != 8 && wv != 9)
         wv = (R->probe_spp > 0 && spp >= R->probe_min_spp) ? 8 : 7;
-    if (S->width == 4 && wv == 8) {
+    if (S->width == 4 && (wv == 8 || wv == 9)) {
         const size_t n_pix = (size_t)R->width * R->height;
         const int tiles_x = (R->width + 7) / 8, n_tiles = tiles_x * ((R->height + 7) / 8);
         if (!R->d_tile_key) {
@@ -2812,10 +2856,25 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
                                per, R->d_order);
             P.order = R->d_order;
         }
-        const int n_wg = R->xcd_bands ? 8 * per : n_tiles;
+        int n_wg = R->xcd_bands ? 8 * per : n_tiles;
+        if (wv == 9) {   // K tiles per wave; pad the order with empty tiles to a multiple of K
+            const int K = std::max(1, R->tiles_per_wave);
+            n_wg = (n_tiles + K - 1) / K;
+            P.tiles_per_wave = K;
+            if (!P.order) {
+                hipLaunchKernelGGL(crt_order_iota_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_order, n_tiles);
+                P.order = R->d_order;
+            }
+            if (n_wg * K > n_tiles)
+                HIP_TRY(hipMemsetAsync(R->d_order + n_tiles, 0xff, (size_t)(n_wg * K - n_tiles) * 4, st));
+        }
         const dim3 tgrid(n_wg), tblock(64);
         const char* cs = cnt ? "true" : "false";
-        if (occ >= 7) {
+        if (wv == 9) {
+            std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 9, 6>", cs);
+            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 9, 6>), tgrid, tblock, 0, st, P);
+            else hipLaunchKernelGGL((crt_render_kernel<false, 9, 6>), tgrid, tblock, 0, st, P);
+        } else if (occ >= 7) {
             std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 8, 7>", cs);
             if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 8, 7>), tgrid, tblock, 0, st, P);
             else hipLaunchKernelGGL((crt_render_kernel<false, 8, 7>), tgrid, tblock, 0, st, P);

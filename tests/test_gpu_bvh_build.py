@@ -116,3 +116,67 @@ def test_bad_index_is_an_error():
     v = np.zeros((3, 3), np.float32)
     with pytest.raises(crt_amd.CrtError):
         crt_amd.build_mesh_bvh(v, np.array([0, 1, 7] * 12, np.uint32), np.zeros(12, np.int32), device=0)
+
+
+# ---- the CRT_BVH_REBUILT binned-SAH tree built on the GPU (crt_scene_options.gpu_build) ----
+
+def _export(hs, gpu):
+    return hs.export("rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=gpu)
+
+
+def _leaf_rank_sets(ex):
+    """Per 4-wide node: the multiset of primitive ranks under its leaf slots (order inside a leaf is free)."""
+    nodes, prims = ex["nodes"].reshape(-1, 8, 4), ex["prims"].reshape(-1, 3, 4)
+    out = []
+    for n in range(ex["nodes_per_layout"]):
+        meta = nodes[n, 6].view(np.int32)
+        first, counts = int(meta[2]), int(meta[3])
+        total = sum((counts >> (8 * s)) & 0xff for s in range(4))
+        out.append(sorted(prims[first:first + total, 2, 2].view(np.int32).tolist()))
+    return out
+
+
+@pytest.mark.parametrize("scene", ["cornell", "cornell_bunny"])
+def test_gpu_sah_tree_equals_host(scenes, scene):
+    """Bin counts and boxes are order-independent, so the GPU build makes the host's splits: same nodes, same
+    boxes, same primitives under every node; only the order inside a leaf may differ (stable partition)."""
+    hs = crt_amd.HostScene(scenes[scene])
+    h, g = _export(hs, False), _export(hs, True)
+    keys = [k for k, v in h.items() if isinstance(v, int)]
+    assert {k: h[k] for k in keys} == {k: g[k] for k in keys}
+    hn, gn = h["nodes"].reshape(-1, 8, 4), g["nodes"].reshape(-1, 8, 4)
+    assert np.array_equal(hn[:, :6], gn[:, :6]), "child boxes"
+    assert np.array_equal(hn[:, 6].view(np.int32), gn[:, 6].view(np.int32)), "node meta"
+    assert _leaf_rank_sets(h) == _leaf_rank_sets(g)
+
+
+def test_gpu_sah_scene_renders_identically(scenes):
+    """Leaf order does not change any hit (closest t, ties to the higher rank): the frames are bit-identical."""
+    hs = crt_amd.HostScene(scenes["cornell_bunny"])
+    a = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0)
+    b = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
+    out = []
+    for sc in (a, b):
+        r = crt_amd.Renderer(160, 90)
+        r.set_camera(crt_amd.camera(16))
+        r.init_rand(41)
+        r.render(sc, 16, 20)
+        r.synchronize()
+        out.append((r.linear(), r.counters()["rays"]))
+    assert np.array_equal(out[0][0].view(np.uint32), out[1][0].view(np.uint32)) and out[0][1] == out[1][1]
+
+
+def test_gpu_sah_million_triangles():
+    from crt_amd import assets
+    hs = crt_amd.HostScene(assets.scene_files("cornell_1m"), build_device=0)
+    t = time.perf_counter()
+    h = _export(hs, False)
+    t_host = time.perf_counter() - t
+    _export(hs, True)   # warm-up
+    t = time.perf_counter()
+    g = _export(hs, True)
+    t_gpu = time.perf_counter() - t
+    assert h["nodes_per_layout"] == g["nodes_per_layout"] and h["prim_float4s"] == g["prim_float4s"]
+    hn, gn = h["nodes"].reshape(-1, 8, 4), g["nodes"].reshape(-1, 8, 4)
+    assert np.array_equal(hn[:, :6], gn[:, :6]) and np.array_equal(hn[:, 6].view(np.int32), gn[:, 6].view(np.int32))
+    print(f"\n1M-triangle rebuilt-scene export: host SAH {t_host * 1e3:.0f} ms, GPU SAH {t_gpu * 1e3:.0f} ms")

@@ -169,7 +169,7 @@ def test_wavefront_equals_megakernel(rebuilt, refill):
 
 
 
-@pytest.mark.parametrize("variant", [7, 8])
+@pytest.mark.parametrize("variant", [7, 8, 9])
 @pytest.mark.parametrize("w,h,spp", [(160, 90, 8), (100, 37, 70), (64, 36, 0)])
 def test_persistent_queue_variant_is_bit_identical(rebuilt, w, h, spp, variant):
     """Variants 7 (lanes take pixels from a global queue in probe-cost order) and 8 (one wave per workgroup, 8x8
@@ -192,7 +192,7 @@ def test_persistent_queue_variant_is_bit_identical(rebuilt, w, h, spp, variant):
     assert np.array_equal(a.rng_state(), b.rng_state())
 
 
-@pytest.mark.parametrize("variant", [7, 8])
+@pytest.mark.parametrize("variant", [7, 8, 9])
 def test_persistent_queue_counting_kernel(rebuilt, variant):
     dev = rebuilt["cornell_bunny", "w4"]
     cam = crt_amd.camera(4)
@@ -222,6 +222,12 @@ def test_xcd_band_order_is_bit_identical(rebuilt, probe_spp):
 def test_first_block_exclusive_is_bit_identical(rebuilt, probe_spp):
     """Variant 7 whose waves refill only after their first 64 pixels are done."""
     _schedule_case(rebuilt, 7, probe_spp, first_block=True)
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_tiles_per_wave_is_bit_identical(rebuilt, k):
+    """Variant 9 with K tiles per wave (78 tiles: K = 3 pads the last wave)."""
+    _schedule_case(rebuilt, 9, 4, tiles_per_wave=k)
 
 
 def _schedule_case(rebuilt, variant, probe_spp, **flags):
