@@ -1793,16 +1793,38 @@ __global__ __launch_bounds__(256) void crt_order_scatter_kernel(const uint32_t* 
         if (i < n) order[h[order_bucket(cost[i])] + rank[k]] = base + (uint32_t)i;
     }
 }
-// Variant 8: the key of an 8x8 tile is its most expensive pixel (the wave ends with its slowest lane).
+// Variant 8: the key of an 8x8 tile is its most expensive pixel (the wave ends with its slowest lane);
+// key_mode 1 adds the mean pixel (ties between tiles with equal maxima); key_mode 2 raises a tile to 3/4 of
+// the largest key among its 8 neighbours (a 4-spp probe underestimates some tiles next to expensive ones, and an
+// underestimated tile dispatched late becomes the launch's tail).
 __global__ void crt_tile_cost_kernel(const uint32_t* __restrict__ pix_cost, int width, int height, int tiles_x,
-                                     int n_tiles, uint32_t* __restrict__ tile_cost) {
+                                     int n_tiles, uint32_t* __restrict__ tile_cost, int key_mode) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tiles) return;
     const int x0 = (t % tiles_x) * 8, y0 = (t / tiles_x) * 8;
-    uint32_t m = 0;
+    uint32_t m = 0, sum = 0, k = 0;
     for (int y = y0; y < min(height, y0 + 8); ++y)
-        for (int x = x0; x < min(width, x0 + 8); ++x) m = max(m, pix_cost[(size_t)y * width + x]);
-    tile_cost[t] = m;
+        for (int x = x0; x < min(width, x0 + 8); ++x) {
+            const uint32_t c = pix_cost[(size_t)y * width + x];
+            m = max(m, c);
+            sum += c;
+            ++k;
+        }
+    tile_cost[t] = key_mode == 1 ? m + sum / max(1u, k) : m;
+}
+__global__ void crt_tile_neighbour_kernel(const uint32_t* __restrict__ key_in, int tiles_x, int n_tiles,
+                                          uint32_t* __restrict__ key_out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_tiles) return;
+    const int tx = t % tiles_x, ty = t / tiles_x, tiles_y = (n_tiles + tiles_x - 1) / tiles_x;
+    uint32_t nb = 0;
+    for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+            const int x = tx + dx, y = ty + dy;
+            if ((dx || dy) && x >= 0 && x < tiles_x && y >= 0 && y < tiles_y && y * tiles_x + x < n_tiles)
+                nb = max(nb, key_in[y * tiles_x + x]);
+        }
+    key_out[t] = max(key_in[t], (nb * 3u) / 4u);
 }
 
 // Variant 8, XCD bands: workgroups are dealt round-robin over the 8 XCDs, so workgroup b runs on the XCD of
@@ -2274,6 +2296,7 @@ struct crt_renderer {
     int xcd_bands = 0;             // variant 8: each XCD renders one horizontal strip (see crt_order_bands_kernel)
     int first_block_exclusive = 0; // variant 7: see RenderParams::first_block_exclusive
     int tiles_per_wave = 2;        // variant 9
+    int tile_key_mode = 0;         // variant 8: see crt_tile_cost_kernel
     uint32_t* d_sorted = nullptr;  // variant 8: tiles sorted per band
     int n_cus = 0;
     int variant = 3;               // see crt_renderer_set_kernel_variant
@@ -2619,6 +2642,7 @@ int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int f
     R->xcd_bands = (flags & 1) ? 1 : 0;
     R->first_block_exclusive = (flags & 2) ? 1 : 0;
     R->tiles_per_wave = ((flags >> 8) & 0xff) ? ((flags >> 8) & 0xff) : 2;
+    R->tile_key_mode = (flags >> 16) & 0xf;
     return CRT_OK;
 }
 
@@ -2829,7 +2853,12 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<true, 4, 6>), grid, block, 0, st, Q);
             else hipLaunchKernelGGL((crt_render_kernel<true, 4, 5>), grid, block, 0, st, Q);
             hipLaunchKernelGGL(crt_tile_cost_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_tile_cost,
-                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key);
+                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode);
+            if (R->tile_key_mode == 2) {   // per-pixel costs are no longer needed: reuse them for the smoothed keys
+                hipLaunchKernelGGL(crt_tile_neighbour_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st,
+                                   R->d_tile_key, tiles_x, n_tiles, R->d_tile_cost);
+                HIP_TRY(hipMemcpyAsync(R->d_tile_key, R->d_tile_cost, (size_t)n_tiles * 4, hipMemcpyDeviceToDevice, st));
+            }
             uint32_t* sorted = R->xcd_bands ? R->d_sorted : R->d_order;
             if (R->xcd_bands && !sorted) {
                 HIP_TRY(hipStreamSynchronize(st));

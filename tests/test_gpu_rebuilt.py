@@ -230,6 +230,11 @@ def test_tiles_per_wave_is_bit_identical(rebuilt, k):
     _schedule_case(rebuilt, 9, 4, tiles_per_wave=k)
 
 
+@pytest.mark.parametrize("key", [1, 2])
+def test_tile_key_modes_are_bit_identical(rebuilt, key):
+    _schedule_case(rebuilt, 8, 4, tile_key=key)
+
+
 def _schedule_case(rebuilt, variant, probe_spp, **flags):
     """A schedule option, with and without the cost probe: the same frame and RNG state as variant 4."""
     dev = rebuilt["cornell_bunny", "w4"]
