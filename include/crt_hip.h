@@ -234,7 +234,8 @@ long long crt_renderer_wavefront_iterations(const crt_renderer* r);   /* iterati
  * workgroup).  Renders with fewer than min_spp samples per pixel skip the probe.  flags: CRT_SCHEDULE_XCD_BANDS
  * (variant 8: each of the 8 XCDs renders one horizontal strip of the image), CRT_SCHEDULE_FIRST_BLOCK (variant 7:
  * a wave's first 64 pixels run without refills), in bits 8-15 the tiles per wave of variant 9 (default 2), in bits
- * 16-19 variant 8's tile key (0 = slowest pixel, 1 = slowest + mean pixel, 2 = 0 raised to 3/4 of the neighbours').
+ * 16-19 variant 8's tile key (0 = slowest pixel, 1 = slowest + mean pixel, 2 = 0 raised to 3/4 of the neighbours';
+ * the renderer starts with 2, the measured best).
  * Default 4, 64, 0; probe_spp 0 disables the probe.  Results never depend on the order. */
 #define CRT_SCHEDULE_XCD_BANDS  1
 #define CRT_SCHEDULE_FIRST_BLOCK 2

@@ -2296,7 +2296,7 @@ struct crt_renderer {
     int xcd_bands = 0;             // variant 8: each XCD renders one horizontal strip (see crt_order_bands_kernel)
     int first_block_exclusive = 0; // variant 7: see RenderParams::first_block_exclusive
     int tiles_per_wave = 2;        // variant 9
-    int tile_key_mode = 0;         // variant 8: see crt_tile_cost_kernel
+    int tile_key_mode = 2;         // variant 8: see crt_tile_cost_kernel (2: measured best, profiles/r01ac)
     uint32_t* d_sorted = nullptr;  // variant 8: tiles sorted per band
     int n_cus = 0;
     int variant = 3;               // see crt_renderer_set_kernel_variant
@@ -2642,7 +2642,7 @@ int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int f
     R->xcd_bands = (flags & 1) ? 1 : 0;
     R->first_block_exclusive = (flags & 2) ? 1 : 0;
     R->tiles_per_wave = ((flags >> 8) & 0xff) ? ((flags >> 8) & 0xff) : 2;
-    R->tile_key_mode = (flags >> 16) & 0xf;
+    R->tile_key_mode = (flags >> 16) & 0xf;   // 0 = slowest pixel (callers that pass 0 get the plain key)
     return CRT_OK;
 }
 
