@@ -236,7 +236,8 @@ long long crt_renderer_wavefront_iterations(const crt_renderer* r);   /* iterati
  * a wave's first 64 pixels run without refills), in bits 8-15 the tiles per wave of variant 9 (default 2), in bits
  * 16-19 variant 8's tile key (0 = slowest pixel, 1 = slowest + mean pixel, 2 = 0 raised to 3/4 of the neighbours';
  * the renderer starts with 2, the measured best).
- * Default 4, 64, 0; probe_spp 0 disables the probe.  Results never depend on the order. */
+ * Default -1 (automatic: 4 probe samples for renders of >= 1000 spp, else 2), 64, 0; probe_spp 0 disables the
+ * probe.  Results never depend on the order. */
 #define CRT_SCHEDULE_XCD_BANDS  1
 #define CRT_SCHEDULE_FIRST_BLOCK 2
 int  crt_renderer_set_schedule(crt_renderer* r, int probe_spp, int min_spp, int flags);

@@ -212,7 +212,7 @@ class Renderer:
     def init_rand(self, seed: int = 41, subsequence_base: int = 0, stream=None):
         check(_lib.hip().crt_renderer_init_rand(self.h, int(seed), int(subsequence_base), stream), "init_rand")
 
-    def set_schedule(self, probe_spp: int = 4, min_spp: int = 64, xcd_bands: bool = False, first_block: bool = False,
+    def set_schedule(self, probe_spp: int = -1, min_spp: int = 64, xcd_bands: bool = False, first_block: bool = False,
                      tiles_per_wave: int = 2, tile_key: int = 2):
         flags = ((1 if xcd_bands else 0) | (2 if first_block else 0) | ((int(tiles_per_wave) & 0xff) << 8)
                  | ((int(tile_key) & 0xf) << 16))

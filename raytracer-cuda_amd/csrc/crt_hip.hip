@@ -2291,7 +2291,8 @@ struct crt_renderer {
     uint32_t* d_tile_cost = nullptr;   // per-pixel probe costs
     uint32_t* d_order_hist = nullptr;
     uint32_t* d_tile_key = nullptr;    // variant 8: per-tile keys
-    int probe_spp = 4;             // samples per pixel of the cost probe (0 = no probe: 8x8-tile order)
+    int probe_spp = -1;            // samples per pixel of the cost probe; 0 = no probe (8x8-tile order),
+                                   // -1 = automatic: 4 for renders of >= 1000 spp, else 2 (profiles/r01ad)
     int probe_min_spp = 64;        // renders with fewer samples per pixel skip the probe
     int xcd_bands = 0;             // variant 8: each XCD renders one horizontal strip (see crt_order_bands_kernel)
     int first_block_exclusive = 0; // variant 7: see RenderParams::first_block_exclusive
@@ -2636,8 +2637,8 @@ int crt_renderer_set_kernel_variant(crt_renderer* R, int variant) {
 }
 
 int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int flags) {
-    if (!R || probe_spp < 0 || probe_spp > 64 || min_spp < 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad schedule");
-    R->probe_spp = probe_spp;
+    if (!R || probe_spp < -1 || probe_spp > 64 || min_spp < 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad schedule");
+    R->probe_spp = probe_spp < 0 ? -1 : probe_spp;
     R->probe_min_spp = min_spp;
     R->xcd_bands = (flags & 1) ? 1 : 0;
     R->first_block_exclusive = (flags & 2) ? 1 : 0;
@@ -2750,6 +2751,12 @@ int crt_renderer_set_wavefront(crt_renderer* R, int refill_lanes, int check_iter
 
 long long crt_renderer_wavefront_iterations(const crt_renderer* R) { return R ? R->wf_iterations : -1; }
 
+// Cost-probe samples for a render of `spp` samples per pixel (0 = no probe).
+static int probe_spp_for(const crt_renderer* R, int spp) {
+    if (spp < R->probe_min_spp || R->probe_spp == 0) return 0;
+    return R->probe_spp > 0 ? R->probe_spp : (spp >= 1000 ? 4 : 2);
+}
+
 int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bounces, unsigned flags, void* stream) {
     if (!R || !S) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
     if (!R->has_camera) return set_error(CRT_ERR_INVALID_ARGUMENT, "camera not set");
@@ -2824,7 +2831,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     // pixel queue) for short renders such as the 1-spp interactive frames
     int wv = R->variant;
     if (S->width == 4 && wv != 4 && wv != 5 && wv != 7 && wv != 8 && wv != 9)
-        wv = (R->probe_spp > 0 && spp >= R->probe_min_spp) ? 8 : 7;
+        wv = probe_spp_for(R, spp) > 0 ? 8 : 7;
     if (S->width == 4 && (wv == 8 || wv == 9)) {
         const size_t n_pix = (size_t)R->width * R->height;
         const int tiles_x = (R->width + 7) / 8, n_tiles = tiles_x * ((R->height + 7) / 8);
@@ -2842,12 +2849,13 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         P.tiles_x = tiles_x;
         P.order = nullptr;
         const int per = (n_tiles + 7) / 8;
-        const bool probe = R->probe_spp > 0 && spp >= R->probe_min_spp;
+        const int pspp = probe_spp_for(R, spp);
+        const bool probe = pspp > 0;
         if (probe) {
             // cost probe (variant 4, read-only) -> slowest pixel per tile -> tiles most expensive first (per XCD
             // band when banded)
             RenderParams Q = P;
-            Q.spp = R->probe_spp;
+            Q.spp = pspp;
             Q.accumulate = 0;
             Q.probe_cost = R->d_tile_cost;
             if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<true, 4, 6>), grid, block, 0, st, Q);
@@ -2929,10 +2937,10 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             HIP_TRY(hipMalloc((void**)&R->d_order_hist, ORDER_KEYS * 4));
             HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
         }
-        if (R->probe_spp > 0 && spp >= R->probe_min_spp) {
+        if (probe_spp_for(R, spp) > 0) {
             // cost probe: variant 4 at probe_spp samples over the same RNG state, read-only: rays per pixel
             RenderParams Q = P;
-            Q.spp = R->probe_spp;
+            Q.spp = probe_spp_for(R, spp);
             Q.accumulate = 0;
             Q.probe_cost = R->d_tile_cost;
             if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<false, 4, 6>), grid, block, 0, st, Q);

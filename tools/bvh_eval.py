@@ -70,7 +70,7 @@ for cfg in a.configs.split(","):
         r.set_occupancy_target(occ)
         r.set_regen_threshold(int(f.get("T", 24)))
         r.set_kernel_variant(int(f.get("V", 3)))
-        r.set_schedule(int(f.get("P", 4)), 64, bool(int(f.get("X", 0))), bool(int(f.get("F", 0))), int(f.get("K", 2)),
+        r.set_schedule(int(f.get("P", -1)), 64, bool(int(f.get("X", 0))), bool(int(f.get("F", 0))), int(f.get("K", 2)),
                        int(f.get("Y", 2)))
         r.set_wavefront(int(f.get("R", 16)), int(f.get("K", 16)))
         t = time.time()
