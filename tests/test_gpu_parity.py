@@ -210,3 +210,24 @@ def test_golden_fixture_frame(device_scenes):
     _, dev = device_scenes["cornell_bunny"]
     r = _render(dev, 64, 36, 16, 20, cam=crt_amd.camera(16))
     _assert_parity(r.linear(), r.rgba8(), g["sum"], g["rgba"], 16)
+
+
+def test_init_rand_cache_returns_the_same_state(device_scenes):
+    """crt_renderer_init_rand keeps the last curand_init array and copies it back for a repeated (seed, base):
+    the state after any sequence of inits and renders equals a fresh renderer's."""
+    w, h = 48, 32
+    _, dev = device_scenes["cornell"]
+    r = crt_amd.Renderer(w, h)
+    r.set_camera(crt_amd.camera(2))
+    fresh = {}
+    for base in (0, 3 * w * h):
+        f = crt_amd.Renderer(w, h)
+        f.init_rand(41, base)
+        fresh[base] = f.rng_state().copy()
+    for base in (0, 0, 3 * w * h, 0, 3 * w * h, 3 * w * h):
+        r.init_rand(41, base)
+        assert np.array_equal(r.rng_state(), fresh[base]), base
+        r.render(dev, 2, 4)          # consumes the stream; the next init must not see it
+        r.synchronize()
+    r.init_rand(42, 0)
+    assert not np.array_equal(r.rng_state(), fresh[0])
