@@ -113,3 +113,23 @@ def test_large_mesh_bvh_matches_oracle(tmp_path):
     lines = ["v %.5f %.5f %.5f\n" % tuple(p) for p in v] + ["f %d %d %d\n" % (3 * k + 1, 3 * k + 2, 3 * k + 3) for k in range(n)]
     p = _write(str(tmp_path), "soup.obj", "".join(lines))
     _compare_scene([p])
+
+
+def test_mesh_builder_abi_matches_scene_pipeline(scenes):
+    """crth_build_mesh_bvh (the host restatement of Mesh::buildBVHMesh as a standalone C entry) builds the same
+    tree and permutation as the scene pipeline, from the loader's unpermuted arrays."""
+    import numpy as np
+    import crt_amd
+    hs = crt_amd.HostScene(scenes["cornell_bunny"])
+    pos, idx, fm, info = hs.loader_arrays()[:4]
+    pidx, pfm = hs.permuted()
+    for i, m in enumerate(info):
+        vo, vc, io, ic, fo = (int(x) for x in m[:5])
+        nodes, oidx, ofm, box, _ = crt_amd.build_mesh_bvh(pos.reshape(-1, 3)[vo:vo + vc], idx[io:io + ic],
+                                                         fm[fo:fo + ic // 3])
+        (boxes, ints), aabb = hs.mesh_bvh(i)
+        assert np.array_equal(np.concatenate([nodes["bmin"], nodes["bmax"]], 1).view(np.uint32), boxes.view(np.uint32))
+        assert np.array_equal(np.stack([nodes[k] for k in ("left", "right", "obj_index", "obj_count", "is_leaf")], 1),
+                              ints)
+        assert np.array_equal(oidx, pidx[io:io + ic]) and np.array_equal(ofm, pfm[fo:fo + ic // 3])
+        assert np.array_equal(box.view(np.uint32), aabb.view(np.uint32))
