@@ -241,8 +241,8 @@ long long crt_renderer_wavefront_iterations(const crt_renderer* r);   /* iterati
 #define CRT_SCHEDULE_XCD_BANDS  1
 #define CRT_SCHEDULE_FIRST_BLOCK 2
 int  crt_renderer_set_schedule(crt_renderer* r, int probe_spp, int min_spp, int flags);
-/* Variants 2-4: number of parked lanes (1..64) that triggers a shading/regeneration pass; default 24 for
- * variants 2/3 and 40 for variant 4 (setting it sets both). */
+/* Variants 2-4, 7-9: number of parked lanes (1..64) that triggers a shading/regeneration pass; default 24 for
+ * variants 2/3 and 44 for the 4-wide variants (setting it sets both). */
 int  crt_renderer_set_regen_threshold(crt_renderer* r, int lanes);
 /* Variant 4: per-lane traversal-stack entries kept in LDS (1..16, default 16); deeper entries spill to a
  * per-pixel region in HBM.  Results do not depend on it (tests force the HBM path with 1). */

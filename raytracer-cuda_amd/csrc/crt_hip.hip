@@ -2307,7 +2307,7 @@ struct crt_renderer {
     unsigned long long diag[3] = {0, 0, 0};
     unsigned long long prof[7] = {0, 0, 0, 0, 0, 0, 0};   // COUNT-mode section profile (variant 4)
     int regen_threshold = 24;      // variants 2/3
-    int regen_threshold_wide = 40; // variant 4 (measured optimum on the 4-wide BVH, profiles/r01d)
+    int regen_threshold_wide = 44; // variants 4/7/8 (measured: 40 for variant 4, profiles/r01d; 44-48 for 8, r01af)
     int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 6 for 4-wide scenes, 5 otherwise
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
     size_t ovf_entries = 0;
