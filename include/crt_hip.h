@@ -308,6 +308,15 @@ int crt_selftest_rcp(uint32_t lo_bits, uint32_t hi_bits, unsigned long long* mis
 /* Wave64 scan self-test: for n_waves x 64 ints, out[3*i..] = DPP inclusive sum, ds_bpermute inclusive sum,
  * DPP inclusive max (per wave of 64 consecutive entries). */
 int crt_selftest_scan(const int* in, int n_waves, int* out);
+/* Known-answer self-test of the render path's primitive functions on the device (tests/golden/primitives.json).
+ * kind 0: Möller–Trumbore (Mesh.cuh:266-308), in 17 floats per record (o3 d3 v0 v1 v2 tmin tmax; tmin is 0.001 in
+ *         the render path), out t or -1;
+ * kind 1: AABB::hit (AABB.cuh:123-146) against [0.001, inf), in 14 floats (o3 d3 lo3 hi3 tmin tmax), out 1 / 0;
+ * kind 2: Sphere::hit (Sphere.cuh:27-47), in 12 floats (o3 d3 center3 radius tmin tmax), out t or -1;
+ * kind 3: Camera::getRay (Camera.cuh:32-44), in 2 ints per pixel (x, y) of a width x height image, rng 6 words per
+ *         pixel (continued in place), out o3 d3. */
+int crt_selftest_geometry(int kind, const float* in, int n, const crt_camera_desc* cam, int width, int height,
+                          uint32_t* rng, float* out);
 /* XORWOW device self-test: init(seed, subseq[i]) then n_draw uniforms per entry. */
 int crt_selftest_rng(unsigned long long seed, const unsigned long long* subseq, int n, int n_draw,
                      uint32_t* state_out /* n*6 */, float* uniforms_out /* n*n_draw */);

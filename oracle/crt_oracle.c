@@ -955,3 +955,60 @@ EXPORT void oracle_camctl_get(const void* p, float* cam19, float* state8) {
     state8[0] = c->yaw; state8[1] = c->pitch; state8[2] = (float)k->moves; state8[3] = (float)k->rotates;
     state8[4] = (float)k->hq; state8[5] = c->focus; state8[6] = (float)k->spp; state8[7] = k->scale;
 }
+
+/* ---- Known-answer entry points for the primitive functions (golden fixtures) ----
+ * Each restates the reference function exactly as the render path uses it. */
+
+/* rayTriangleIntersect (Mesh.cuh:266-308) on n records of 17 floats: o3 d3 v0 3 v1 3 v2 3 tmin tmax.
+ * out: t, or -1 when rejected. */
+EXPORT void oracle_kat_triangle(const float* in, int n, float* out) {
+    static const Mesh none;
+    for (int i = 0; i < n; i++) {
+        const float* q = in + 17 * i;
+        Ray r; r.o = v3(q[0], q[1], q[2]); r.d = v3(q[3], q[4], q[5]);
+        Hit h;
+        Mesh m = none;
+        int32_t fm = 0;
+        m.fmat = &fm;
+        out[i] = tri_hit(&m, &r, v3(q[6], q[7], q[8]), v3(q[9], q[10], q[11]), v3(q[12], q[13], q[14]),
+                         iv(q[15], q[16]), &h, 0) ? h.t : -1.f;
+    }
+}
+
+/* AABB::hit (AABB.cuh:123-146) on n records of 14 floats: o3 d3 lo3 hi3 tmin tmax (the box as stored, no
+ * padding applied here).  out: 1 hit / 0 miss. */
+EXPORT void oracle_kat_box(const float* in, int n, int* out) {
+    for (int i = 0; i < n; i++) {
+        const float* q = in + 14 * i;
+        Ray r; r.o = v3(q[0], q[1], q[2]); r.d = v3(q[3], q[4], q[5]);
+        Box b; b.x = iv(q[6], q[9]); b.y = iv(q[7], q[10]); b.z = iv(q[8], q[11]);
+        out[i] = box_hit(&b, &r, iv(q[12], q[13]));
+    }
+}
+
+/* Sphere::hit (Sphere.cuh:27-47) on n records of 12 floats: o3 d3 center3 radius tmin tmax.  out: t or -1. */
+EXPORT void oracle_kat_sphere(const float* in, int n, float* out) {
+    for (int i = 0; i < n; i++) {
+        const float* q = in + 12 * i;
+        Ray r; r.o = v3(q[0], q[1], q[2]); r.d = v3(q[3], q[4], q[5]);
+        Sphere s = make_sphere(v3(q[6], q[7], q[8]), q[9], 0);
+        Hit h;
+        out[i] = sphere_hit(&s, &r, iv(q[10], q[11]), &h) ? h.t : -1.f;
+    }
+}
+
+/* Camera::getRay (Camera.cuh:32-44) for n pixels (xy[2i], xy[2i+1]) of a w x h image; rng: 6 words per
+ * pixel, continued in place.  out: o3 d3 per pixel. */
+EXPORT void oracle_kat_get_ray(const float* cam19, int w, int h, const int* xy, uint32_t* rng, int n, float* out) {
+    Cam c; memset(&c, 0, sizeof c);
+    memcpy(c.pos.e, cam19, 12); memcpy(c.llc.e, cam19 + 3, 12); memcpy(c.horiz.e, cam19 + 6, 12);
+    memcpy(c.vert.e, cam19 + 9, 12); memcpy(c.right.e, cam19 + 12, 12); memcpy(c.up.e, cam19 + 15, 12);
+    c.lens_r = cam19[18];
+    for (int i = 0; i < n; i++) {
+        Rng s; memcpy(&s, rng + 6 * i, sizeof s);
+        Ray r = cam_get_ray(&c, xy[2 * i], xy[2 * i + 1], w, h, &s);
+        memcpy(rng + 6 * i, &s, sizeof s);
+        memcpy(out + 6 * i, r.o.e, 12);
+        memcpy(out + 6 * i + 3, r.d.e, 12);
+    }
+}

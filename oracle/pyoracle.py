@@ -178,3 +178,49 @@ def seq_matrix(k: int) -> np.ndarray:
     out = np.zeros(800, np.uint32)
     lib().oracle_seq_matrix(k, _p(out))
     return out
+
+
+def _kat_lib():
+    L = lib()
+    if not getattr(L, "_kat_bound", False):
+        P, i32 = C.c_void_p, C.c_int
+        L.oracle_kat_triangle.argtypes = [P, i32, P]
+        L.oracle_kat_box.argtypes = [P, i32, P]
+        L.oracle_kat_sphere.argtypes = [P, i32, P]
+        L.oracle_kat_get_ray.argtypes = [P, i32, i32, P, P, i32, P]
+        L._kat_bound = True
+    return L
+
+
+def kat_triangle(rec: np.ndarray) -> np.ndarray:
+    """rayTriangleIntersect on (n, 17) f32 records o3 d3 v0 v1 v2 tmin tmax -> t or -1 (crt_oracle.c)."""
+    rec = np.ascontiguousarray(rec, np.float32)
+    out = np.zeros(len(rec), np.float32)
+    _kat_lib().oracle_kat_triangle(_p(rec), len(rec), _p(out))
+    return out
+
+
+def kat_box(rec: np.ndarray) -> np.ndarray:
+    """AABB::hit on (n, 14) f32 records o3 d3 lo3 hi3 tmin tmax -> 1 / 0."""
+    rec = np.ascontiguousarray(rec, np.float32)
+    out = np.zeros(len(rec), np.int32)
+    _kat_lib().oracle_kat_box(_p(rec), len(rec), _p(out))
+    return out
+
+
+def kat_sphere(rec: np.ndarray) -> np.ndarray:
+    """Sphere::hit on (n, 12) f32 records o3 d3 centre3 radius tmin tmax -> t or -1."""
+    rec = np.ascontiguousarray(rec, np.float32)
+    out = np.zeros(len(rec), np.float32)
+    _kat_lib().oracle_kat_sphere(_p(rec), len(rec), _p(out))
+    return out
+
+
+def kat_get_ray(cam19: np.ndarray, w: int, h: int, xy: np.ndarray, rng: np.ndarray) -> np.ndarray:
+    """Camera::getRay for pixels xy (n, 2); rng (n, 6) u32 is continued in place.  Returns (n, 6) o3 d3."""
+    cam19 = np.ascontiguousarray(cam19, np.float32)
+    xy = np.ascontiguousarray(xy, np.int32)
+    assert rng.dtype == np.uint32 and rng.flags.c_contiguous and rng.shape == (len(xy), 6)
+    out = np.zeros((len(xy), 6), np.float32)
+    _kat_lib().oracle_kat_get_ray(_p(cam19), w, h, _p(xy), _p(rng), len(xy), _p(out))
+    return out

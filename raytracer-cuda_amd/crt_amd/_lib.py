@@ -98,7 +98,7 @@ HIP_SYMBOLS = [
     "crt_renderer_attach_linear", "crt_renderer_set_kernel_variant", "crt_renderer_get_schedule_stats",
     "crt_renderer_set_regen_threshold", "crt_renderer_set_occupancy_target",
     "crt_build_mesh_bvh", "crt_renderer_set_schedule",
-    "crt_selftest_math", "crt_selftest_rng", "crt_selftest_scan", "crt_selftest_rcp",
+    "crt_selftest_math", "crt_selftest_rng", "crt_selftest_geometry", "crt_selftest_scan", "crt_selftest_rcp",
 ]
 HOST_SYMBOLS = [
     "crth_scene_load", "crth_scene_load_ex", "crth_scene_build_ms", "crth_scene_destroy", "crth_scene_desc", "crth_scene_upload", "crth_scene_upload_ex", "crth_scene_counts",
@@ -164,6 +164,7 @@ def hip():
             "crt_renderer_set_schedule": ([P, i32, i32], i32),
             "crt_build_mesh_bvh": ([i32, P, C.c_uint32, P, P, C.c_uint32, P, P, P, P], i32),
             "crt_selftest_math": ([P, P, i32, P, P], i32),
+            "crt_selftest_geometry": ([i32, P, i32, P, i32, i32, P, P], i32),
             "crt_selftest_rng": ([u64, P, i32, i32, P, P], i32),
             "crt_selftest_scan": ([P, i32, P], i32),
             "crt_selftest_rcp": ([C.c_uint32, C.c_uint32, P, P], i32),

@@ -1733,6 +1733,56 @@ __global__ __launch_bounds__(64) void crt_selftest_scan_kernel(const int* in, in
     out[3 * (64 * w + lane) + 2] = (int)wave_inclusive_max_scan_u((uint32_t)(x + 1)) - 1;
 }
 
+// Known-answer self-test of the render path's own primitive functions (tests/golden/primitives.json):
+// kind 0 = tri_test_rec (Möller–Trumbore, window [0.001, tmax]), 1 = ref_scene_box (AABB::hit against
+// [0.001, inf) with the exact 1/d), 2 = sphere_candidate (Sphere::hit, window [0.001, tmax]), 3 = next_ray's
+// Camera::getRay for a new sample.
+__global__ void crt_selftest_geometry_kernel(int kind, const float* __restrict__ in, int n, float* __restrict__ out,
+                                             uint32_t* __restrict__ rng, crt_camera_desc cam, int w, int h) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (kind == 0) {
+        const float* q = in + 17 * i;
+        const V3 o = v3(q[0], q[1], q[2]), d = v3(q[3], q[4], q[5]);
+        const float e1[3] = {q[9] - q[6], q[10] - q[7], q[11] - q[8]}, e2[3] = {q[12] - q[6], q[13] - q[7], q[14] - q[8]};
+        const float4 f0 = make_float4(q[6], q[7], q[8], e1[0]), f1 = make_float4(e1[1], e1[2], e2[0], e2[1]);
+        const float4 f2 = make_float4(e2[2], 0.f, 0.f, 0.f);
+        out[i] = tri_test_rec(f0, f1, f2, o, d, q[16]);
+    } else if (kind == 1) {
+        const float* q = in + 14 * i;
+        const V3 o = v3(q[0], q[1], q[2]), d = v3(q[3], q[4], q[5]);
+        const V3 inv = v3(recip_exact_any(d.x), recip_exact_any(d.y), recip_exact_any(d.z));
+        out[i] = ref_scene_box(make_float4(q[6], q[7], q[8], q[9]), make_float4(q[10], q[11], 0.f, 0.f), o, inv) ? 1.f : 0.f;
+    } else if (kind == 2) {
+        const float* q = in + 12 * i;
+        const V3 o = v3(q[0], q[1], q[2]), d = v3(q[3], q[4], q[5]);
+        out[i] = sphere_candidate(make_float4(q[6], q[7], q[8], q[9]), make_float4(q[9] * q[9], 0.f, 0.f, 0.f), o, d,
+                                  q[11]);
+    } else {
+        const int* xy = reinterpret_cast<const int*>(in);
+        CamRegs C;
+        C.pos = v3(cam.origin[0], cam.origin[1], cam.origin[2]);
+        C.llc = v3(cam.lower_left[0], cam.lower_left[1], cam.lower_left[2]);
+        C.hor = v3(cam.horizontal[0], cam.horizontal[1], cam.horizontal[2]);
+        C.ver = v3(cam.vertical[0], cam.vertical[1], cam.vertical[2]);
+        C.right = v3(cam.right[0], cam.right[1], cam.right[2]);
+        C.up = v3(cam.up[0], cam.up[1], cam.up[2]);
+        C.lens = cam.lens_radius;
+        C.fw = (float)w;
+        C.fh = (float)h;
+        PathState S;
+        uint32_t* r = rng + 6 * (size_t)i;
+        S.s = Rng{r[0], r[1], r[2], r[3], r[4], r[5]};
+        S.pixel = v3(0.f, 0.f, 0.f);
+        S.thr = v3(1.f, 1.f, 1.f);
+        S.remaining = 1; S.bounce = 0; S.need_new = true; S.rays = 0; S.paths = 0;
+        next_ray(S, C, xy[2 * i], xy[2 * i + 1], 20);
+        r[0] = S.s.v0; r[1] = S.s.v1; r[2] = S.s.v2; r[3] = S.s.v3; r[4] = S.s.v4; r[5] = S.s.d;
+        float* o6 = out + 6 * (size_t)i;
+        o6[0] = S.o.x; o6[1] = S.o.y; o6[2] = S.o.z; o6[3] = S.d.x; o6[4] = S.d.y; o6[5] = S.d.z;
+    }
+}
+
 __global__ void crt_selftest_rng_kernel(const uint32_t* st_in, int n, int n_draw, float* out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -3223,6 +3273,33 @@ int crt_selftest_scan(const int* in, int n_waves, int* out) {
     HIP_TRY(hipMemcpy(out, dout, (size_t)n_waves * 64 * 12, hipMemcpyDeviceToHost));
     (void)hipFree(din);
     (void)hipFree(dout);
+    return CRT_OK;
+}
+
+int crt_selftest_geometry(int kind, const float* in, int n, const crt_camera_desc* cam, int width, int height,
+                          uint32_t* rng, float* out) {
+    static const int in_words[4] = {17, 14, 12, 2}, out_words[4] = {1, 1, 1, 6};
+    if (kind < 0 || kind > 3 || !in || !out || n <= 0 || (kind == 3 && (!cam || !rng || width <= 0 || height <= 0)))
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    if (int rc = use_device(0)) return rc;
+    float *din, *dout;
+    uint32_t* drng = nullptr;
+    HIP_TRY(hipMalloc((void**)&din, (size_t)n * in_words[kind] * 4));
+    HIP_TRY(hipMalloc((void**)&dout, (size_t)n * out_words[kind] * 4));
+    if (kind == 3) HIP_TRY(hipMalloc((void**)&drng, (size_t)n * 24));
+    hipError_t e = hipMemcpy(din, in, (size_t)n * in_words[kind] * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess && kind == 3) e = hipMemcpy(drng, rng, (size_t)n * 24, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(crt_selftest_geometry_kernel, dim3((n + 63) / 64), dim3(64), 0, 0, kind, din, n, dout, drng,
+                           cam ? *cam : crt_camera_desc{}, width, height);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * out_words[kind] * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && kind == 3) e = hipMemcpy(rng, drng, (size_t)n * 24, hipMemcpyDeviceToHost);
+    (void)hipFree(din);
+    (void)hipFree(dout);
+    if (drng) (void)hipFree(drng);
+    HIP_TRY(e);
     return CRT_OK;
 }
 

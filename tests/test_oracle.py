@@ -74,6 +74,21 @@ def test_cornell_bunny_golden_frame(oracle_scenes):
     assert c["rays"] == meta["rays"] and c["tri_tests"] == meta["tri_tests"]
 
 
+def test_config_e_slice_golden_frame():
+    """Config E's 1M-triangle scene (instanced bunnies) at 64x36, 8 spp: the oracle reproduces the committed
+    fixture (sums, RGBA8, ray count); the GPU suite holds both BVH paths to the same file."""
+    from crt_amd import assets
+    import hashlib
+    g = np.load(GOLDEN / "cornell_1m_64x36_8spp.npz")
+    S = pyoracle.OracleScene(objload.load_scene(assets.scene_files("cornell_1m")))
+    s, rgba, c = S.render(pyoracle.camera(), 64, 36, 8, 20)
+    assert np.array_equal(s.view(np.uint32), g["sum"].view(np.uint32))
+    assert np.array_equal(rgba, g["rgba"])
+    meta = json.loads((GOLDEN / "frames.json").read_text())["cornell_1m_64x36_8spp_20b"]
+    assert c["rays"] == int(g["rays"][0]) == meta["rays"]
+    assert hashlib.sha256(s.tobytes()).hexdigest() == meta["sum_sha256"]
+
+
 def test_bvh_golden(scenes, oracle_scenes):
     g = json.loads((GOLDEN / "scene_bvh.json").read_text())
     S = oracle_scenes["cornell"]
