@@ -587,9 +587,28 @@ __device__ __forceinline__ float sphere_root(float qa, float hb, float disc) {
     return root;
 }
 
+// The per-ray spheres of the 4-wide variants are tested after the trace, against the trace's closest hit (the hit
+// rule is order-independent, so the result is the same as testing them first).  A sphere whose near root is
+// provably beyond that hit then skips the correctly rounded sqrt and division: with su >= sqrtf(disc) (raw
+// v_sqrt_f32 is within 1 ulp, so 4 ulp of margin), fl(-hb - su) <= fl(-hb - sqrtf(disc)) by monotone rounding, and
+// fl(-hb - su) > fl(closest * qa) * (1 + 1e-5) puts the exact root above nextafter(closest).  The far root is
+// larger still.  -DCRT_RAY_SPHERES_FIRST restores the test at ray start (A/B builds).
+#ifdef CRT_RAY_SPHERES_FIRST
+#define CRT_SPHERES_LATE 0
+#else
+#define CRT_SPHERES_LATE 1
+#endif
+__device__ __forceinline__ bool sphere_beyond(float qa, float hb, float disc, float closest) {
+    if (!(disc > 1e-30f) || !(closest < __builtin_inff())) return false;
+    const float su = __builtin_amdgcn_sqrtf(disc) * (1.0f + 0x1p-21f);
+    const float lb = -hb - su;
+    return lb > (closest * qa) * (1.0f + 1e-5f);
+}
+
 // Two spheres at once (data from the kernel arguments): the reference box tests and the discriminant
 // arithmetic in packed f32 (IEEE per half, the reference's operation order: (x*x + y*y) + z*z), roots and
 // divisions per sphere.
+template <bool LATE = false>
 __device__ __forceinline__ void ray_spheres2(const float* sa, const float* sb, V3 o, V3 d, V3 inv,
                                              float& closest, int& hit) {
     const pf2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
@@ -613,14 +632,15 @@ __device__ __forceinline__ void ray_spheres2(const float* sa, const float* sb, V
     const pf2 qc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - (pf2){sa[3], sb[3]};
     const pf2 qa2 = {qa, qa};
     const pf2 disc = hb * hb - qa2 * qc;
-    const float ta = reach[0] ? sphere_root(qa, hb.x, disc.x) : -1.f;
-    const float tb = reach[1] ? sphere_root(qa, hb.y, disc.y) : -1.f;
+    const float ta = reach[0] && !(LATE && sphere_beyond(qa, hb.x, disc.x, closest)) ? sphere_root(qa, hb.x, disc.x) : -1.f;
+    const float tb = reach[1] && !(LATE && sphere_beyond(qa, hb.y, disc.y, closest)) ? sphere_root(qa, hb.y, disc.y) : -1.f;
     const int ra = __float_as_int(sa[4]), rb = __float_as_int(sb[4]);
     if (ta >= 0.f && better(ta, ra, closest, hit)) { closest = ta; hit = ra; }
     if (tb >= 0.f && better(tb, rb, closest, hit)) { closest = tb; hit = rb; }
 }
 
 // inv: AABB::hit's 1/d, bit-exact (recip_exact_any), shared with the traversal.
+template <bool LATE = false>
 __device__ __forceinline__ void ray_spheres(const float4* __restrict__ prims, const float4* __restrict__ chain,
                                             int n_chain, int first, int n, V3 o, V3 d, V3 inv, float& closest,
                                             int& hit, const float* sph2 = nullptr) {
@@ -629,7 +649,7 @@ __device__ __forceinline__ void ray_spheres(const float4* __restrict__ prims, co
     return;   // profiling build only (tools/build_profile_lib.sh): measures what the per-ray sphere tests cost
 #endif
     if (n == 2 && sph2) {
-        ray_spheres2(sph2, sph2 + 12, o, d, inv, closest, hit);
+        ray_spheres2<LATE>(sph2, sph2 + 12, o, d, inv, closest, hit);
         return;
     }
     for (int s = 0; s < n; ++s) {
@@ -916,8 +936,12 @@ __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int h
         ++S.bounce;
         return;
     }
+    // Lambertian and Metal both draw one randomUnitVector first (their only draws): one rejection loop for
+    // both, so a wave holding both materials does not run the loop twice.
+    V3 ruv;
+    if (code == SHADE_LAMBERT || code == SHADE_METAL) ruv = rand_unit_vector(S.s);
     if (code == SHADE_LAMBERT) {                         // Material.cuh:66-77
-        V3 sd = n + rand_unit_vector(S.s);
+        V3 sd = n + ruv;
         if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = n;
         S.thr = S.thr * v3(m.x, m.y, m.z);
         S.o = hp;
@@ -925,7 +949,7 @@ __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int h
         ++S.bounce;
     } else if (code == SHADE_METAL) {                    // :89-96
         V3 refl = reflect(S.d, n);
-        refl = unit(refl) + (m.w * rand_unit_vector(S.s));
+        refl = unit(refl) + (m.w * ruv);
         if (dot(refl, n) > 0) {
             S.thr = S.thr * v3(m.x, m.y, m.z);
             S.o = hp;
@@ -1073,6 +1097,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             if (n_parked >= P.regen_threshold || n_parked == n_live) {
                 if (COUNT) cnt.passes++;
                 if (parked) {
+                    if (CRT_SPHERES_LATE && has_result)
+                        ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
+                                          inv, closest, hit, sph_lds);
                     if (has_result) shade(S, P, hit, closest);
                     live = next_ray(S, C, px, py, P.max_bounces);
                     has_result = false;
@@ -1152,8 +1179,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
 #else
                     inv = v3(recip_exact_any(S.d.x), recip_exact_any(S.d.y), recip_exact_any(S.d.z));
 #endif
-                    ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d, inv,
-                                closest, hit, sph_lds);
+                    if (!CRT_SPHERES_LATE)
+                        ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d, inv,
+                                    closest, hit, sph_lds);
                     if (COUNT) cnt.spheres += P.n_ray_spheres;
                     L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                     if (COUNT) cnt.trace_calls++;
@@ -1184,6 +1212,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 if (COUNT) cnt.passes++;
                 if (parked) {
                     const uint64_t s0 = COUNT ? shader_clock() : 0;
+                    if (CRT_SPHERES_LATE && has_result)
+                        ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
+                                          inv, closest, hit, sph_lds);
                     if (has_result) shade(S, P, hit, closest);
                     const uint64_t s1 = COUNT ? shader_clock() : 0;
                     live = next_ray(S, C, x, y, P.max_bounces);
@@ -1207,8 +1238,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
 #else
                         inv = v3(recip_exact_any(S.d.x), recip_exact_any(S.d.y), recip_exact_any(S.d.z));
 #endif
-                        ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d, inv,
-                                    closest, hit, sph_lds);
+                        if (!CRT_SPHERES_LATE)
+                            ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
+                                        inv, closest, hit, sph_lds);
                         if (COUNT) cnt.spheres += P.n_ray_spheres;
                         L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                         if (COUNT) cnt.trace_calls++;
