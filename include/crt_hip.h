@@ -314,7 +314,9 @@ int crt_selftest_scan(const int* in, int n_waves, int* out);
  * kind 1: AABB::hit (AABB.cuh:123-146) against [0.001, inf), in 14 floats (o3 d3 lo3 hi3 tmin tmax), out 1 / 0;
  * kind 2: Sphere::hit (Sphere.cuh:27-47), in 12 floats (o3 d3 center3 radius tmin tmax), out t or -1;
  * kind 3: Camera::getRay (Camera.cuh:32-44), in 2 ints per pixel (x, y) of a width x height image, rng 6 words per
- *         pixel (continued in place), out o3 d3. */
+ *         pixel (continued in place), out o3 d3;
+ * kind 4: the per-ray spheres' skip test (a root provably beyond the trace's closest hit), in 12 floats (o3 d3
+ *         center3 radius closest unused), out 1 = skipped / 0 = tested exactly. */
 int crt_selftest_geometry(int kind, const float* in, int n, const crt_camera_desc* cam, int width, int height,
                           uint32_t* rng, float* out);
 /* XORWOW device self-test: init(seed, subseq[i]) then n_draw uniforms per entry. */

@@ -1790,6 +1790,14 @@ __global__ void crt_selftest_geometry_kernel(int kind, const float* __restrict__
         const V3 o = v3(q[0], q[1], q[2]), d = v3(q[3], q[4], q[5]);
         out[i] = sphere_candidate(make_float4(q[6], q[7], q[8], q[9]), make_float4(q[9] * q[9], 0.f, 0.f, 0.f), o, d,
                                   q[11]);
+    } else if (kind == 4) {   // the per-ray spheres' skip test (sphere_beyond) against closest = q[10]
+        const float* q = in + 12 * i;
+        const float ocx = q[0] - q[6], ocy = q[1] - q[7], ocz = q[2] - q[8];
+        const float qa = dot(v3(q[3], q[4], q[5]), v3(q[3], q[4], q[5]));
+        const float hb = (ocx * q[3] + ocy * q[4]) + ocz * q[5];
+        const float qc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - q[9] * q[9];
+        const float disc = hb * hb - qa * qc;
+        out[i] = sphere_beyond(qa, hb, disc, q[10]) ? 1.f : 0.f;
     } else {
         const int* xy = reinterpret_cast<const int*>(in);
         CamRegs C;
@@ -3310,8 +3318,8 @@ int crt_selftest_scan(const int* in, int n_waves, int* out) {
 
 int crt_selftest_geometry(int kind, const float* in, int n, const crt_camera_desc* cam, int width, int height,
                           uint32_t* rng, float* out) {
-    static const int in_words[4] = {17, 14, 12, 2}, out_words[4] = {1, 1, 1, 6};
-    if (kind < 0 || kind > 3 || !in || !out || n <= 0 || (kind == 3 && (!cam || !rng || width <= 0 || height <= 0)))
+    static const int in_words[5] = {17, 14, 12, 2, 12}, out_words[5] = {1, 1, 1, 6, 1};
+    if (kind < 0 || kind > 4 || !in || !out || n <= 0 || (kind == 3 && (!cam || !rng || width <= 0 || height <= 0)))
         return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
     if (int rc = use_device(0)) return rc;
     float *din, *dout;

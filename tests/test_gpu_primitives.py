@@ -2,7 +2,7 @@
 
 * tests/golden/primitives.json: crt_selftest_geometry runs the records through the device functions the render
   kernels call (tri_test_rec, ref_scene_box with the exact 1/d, sphere_candidate, next_ray's getRay) and must
-  return the oracle's f32 words bit for bit.
+  return the oracle's f32 words bit for bit.  Kind 4 checks the per-ray spheres' skip test against the oracle's roots.
 * tests/golden/cornell_1m_64x36_8spp.npz: the 1M-triangle scene (config E's, instanced bunnies) rendered by the
   oracle.  The reference-BVH path must match it bit for bit including the ray count; the benchmarked rebuilt
   4-wide path within the north-star RMS.
@@ -110,3 +110,39 @@ def test_config_e_slice_rebuilt_within_rms(million, variant):
     assert (rms <= RMS_TOL).all(), f"per-channel RMS {rms}"
     eq = np.mean(np.all(lin.view(np.uint32) == g["sum"].view(np.uint32), axis=-1))
     assert eq >= 0.95, f"only {eq:.4f} of pixels bit-identical"
+
+
+def test_device_sphere_skip_never_drops_a_winner(kat):
+    """The per-ray spheres run after the trace and skip the exact root when it is provably beyond the trace's
+    closest hit (sphere_beyond).  For closest values at and around each record's exact root (nextafter steps, 1e-6
+    and 1e-5 relative, far away), a skipped record's accepted root (oracle, tmax = inf) is strictly beyond closest."""
+    import pyoracle
+    rec = unhex(kat["sphere"]["in_hex"], 12).copy()
+    rec[:, 10], rec[:, 11] = np.float32(0.001), np.float32(np.inf)
+    t = pyoracle.kat_sphere(rec)
+    hit = rec[t >= 0]
+    th = t[t >= 0]
+    cands = [th]
+    for k in range(1, 9):
+        up, dn = th.copy(), th.copy()
+        for _ in range(k):
+            up = np.nextafter(up, np.float32(np.inf))
+            dn = np.nextafter(dn, np.float32(0))
+        cands += [up, dn]
+    for f in (1 - 1e-5, 1 - 1e-6, 1 + 1e-6, 1 + 1e-5, 1 + 2e-5, 1 + 1e-4, 2.0, 0.5):
+        cands.append((th * np.float32(f)).astype(np.float32))
+    rows, roots = [], []
+    for c in cands:
+        r = hit.copy()
+        r[:, 10] = c
+        rows.append(r)
+        roots.append(th)
+    rows, roots = np.concatenate(rows), np.concatenate(roots)
+    skipped = _geometry(4, rows) == 1
+    assert skipped.any() and not skipped.all()
+    bad = skipped & ~(roots > rows[:, 10])
+    assert not bad.any(), f"{bad.sum()} records skipped with root <= closest"
+    # closest = inf (no triangle hit) never skips
+    r = hit.copy()
+    r[:, 10] = np.inf
+    assert not (_geometry(4, r) == 1).any()
