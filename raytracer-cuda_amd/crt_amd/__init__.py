@@ -330,8 +330,9 @@ class Renderer:
 
 
 def pixel_sample_scale(spp: int) -> float:
-    """m_PixelSampleScale = 1.f / m_SamplesPerPixel (Camera.cuh:23), rounded to f32."""
-    return float(np.float32(1.0) / np.float32(spp))
+    """m_PixelSampleScale = 1.f / m_SamplesPerPixel (Camera.cuh:23), rounded to f32 (spp 0 gives inf, as in C)."""
+    with np.errstate(divide="ignore"):
+        return float(np.float32(1.0) / np.float32(spp))
 
 
 def device_count() -> int:

@@ -170,12 +170,13 @@ def test_wavefront_equals_megakernel(rebuilt, refill):
 
 
 @pytest.mark.parametrize("variant", [7, 8, 9])
-@pytest.mark.parametrize("w,h,spp", [(160, 90, 8), (100, 37, 70), (64, 36, 0)])
+@pytest.mark.parametrize("w,h,spp", [(160, 90, 8), (100, 37, 70), (64, 36, 0), (1, 1, 64), (9, 1, 65), (1, 17, 3)])
 def test_persistent_queue_variant_is_bit_identical(rebuilt, w, h, spp, variant):
     """Variants 7 (lanes take pixels from a global queue in probe-cost order) and 8 (one wave per workgroup, 8x8
     tiles in probe-cost order) trace every pixel with ONE lane, samples in order, from its own RNG stream: the
     frame, the RNG state and the ray count equal variant 4's.  spp 70 >= 64 runs the cost probe and the sorted
-    order; 8 uses row-major order; 0 traces nothing.  100x37 has partial 8x8 tiles."""
+    order; 8 uses row-major order; 0 traces nothing.  100x37 has partial 8x8 tiles; 1x1, 9x1 and 1x17 are
+    degenerate frames (one partial tile, a partial tile row / column)."""
     dev = rebuilt["cornell_bunny", "w4"]
     cam = crt_amd.camera(max(spp, 1))
     a = _frame(dev, w, h, spp, 20, cam, variant=4)
