@@ -743,18 +743,19 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
         const uint32_t counts = __float_as_uint(mf.w);
         const int n_int = meta & 0xff;
         if (COUNT) cnt.boxes += (uint32_t)(meta >> 8);
-        // leaf children: consecutive primitives; test the span from the first to the last hit leaf
-        const int c0 = counts & 0xff, c1 = (counts >> 8) & 0xff, c2 = (counts >> 16) & 0xff, c3 = counts >> 24;
-        const int off[4] = {0, c0, c0 + c1, c0 + c1 + c2};
-        const int cc[4] = {c0, c1, c2, c3};
-        int lo = 0x7fffffff, hi = 0;
+        // leaf children: consecutive primitives; test the span from the first to the last hit leaf.  Slots
+        // [n_int, n_slots) are leaves (count >= 1), empty slots are never hit, so the hit leaves are the hit bits
+        // above n_int; counts * 0x01010101 holds the running ends in its bytes (at most 255 primitives per node,
+        // checked by the builder).
+        uint32_t hm = 0;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const bool lh = s >= n_int && cc[s] > 0 && w.hit[s];
-            lo = lh ? min(lo, off[s]) : lo;
-            hi = lh ? max(hi, off[s] + cc[s]) : hi;
-        }
-        if (hi > lo) {
+        for (int s = 0; s < 4; ++s) hm |= w.hit[s] ? (1u << s) : 0u;
+        const uint32_t lm = hm & (0xfu << n_int);
+        if (lm) {
+            const uint32_t ends = counts * 0x01010101u;
+            const uint32_t first = (uint32_t)__builtin_ctz(lm), last = 31u - (uint32_t)__builtin_clz(lm);
+            const int lo = (int)(((ends << 8) >> (8u * first)) & 0xffu);
+            const int hi = (int)((ends >> (8u * last)) & 0xffu);
             leaf_n = hi - lo;
             leaf_first = __float_as_int(mf.z) + lo;
         }
@@ -2274,10 +2275,12 @@ private:
             for (int s = 0; s < w.n_internal; ++s) queue.push_back(w.bin[s]);
             const int leaf_first = (int)(prims.size() / 3);
             uint32_t counts = 0;
+            int total_leaf = 0;
             for (int s = w.n_internal; s < w.n_slots; ++s) {
                 const crt_sah::Node& L = bn[w.bin[s]];
                 if (L.count > 255) { err = "leaf too large"; return false; }
                 counts |= (uint32_t)L.count << (8 * s);
+                total_leaf += L.count;
                 for (int i = L.first; i < L.first + L.count; ++i) {
                     const int src = its[i].src, np = (int)(prims.size() / 3);
                     for (int q = 0; q < 3; ++q) prims.push_back(F.prims[3 * src + q]);
@@ -2285,6 +2288,8 @@ private:
                 }
             }
             if (prims.size() / 3 >= (size_t)SPHERE_BIT) { err = "too many primitives"; return false; }
+            // node_step4 takes the leaf span from counts * 0x01010101 (byte-wise running sums)
+            if (total_leaf > 255) { err = "leaf children of one node hold more than 255 primitives"; return false; }
             float row[6][4];
             for (int s = 0; s < 4; ++s) {
                 for (int a = 0; a < 3; ++a) {
