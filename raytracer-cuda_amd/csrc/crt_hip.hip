@@ -728,6 +728,15 @@ __device__ __forceinline__ uint32_t* ovf_slot(const RenderParams& P, int at, siz
     return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(P.ovf) + byte);
 }
 
+// The lane id recomputed at the point of use (two VALU ops, no register kept across the loop): at the 80-VGPR
+// budget of 6 waves/SIMD the allocator otherwise spills the lane's stack address and reloads it from scratch on
+// every push and pop.
+__device__ __forceinline__ int lane_fresh() {
+    int l;
+    __asm__ volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, int& node, int& sp, float closest,
                                            TraceCounts& cnt, uint32_t* __restrict__ stk, int lane, size_t pix,
@@ -737,6 +746,9 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
     if (node >= 0) {
         const float4* q = P.nodes + 8 * (size_t)node;
         const float4 mf = q[6];
+        // keep the whole link row in the node's loads: left to itself the compiler loads leaf_first / counts
+        // only inside the leaf branch, one more dependent load on a leaf step's critical path
+        __asm__ volatile("" : : "v"(mf.z), "v"(mf.w));
         const Wide4 w = wide_boxes(q, o, inv, closest);
         const int first_child = __float_as_int(mf.x);
         const int meta = __float_as_int(mf.y);
@@ -764,7 +776,7 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
         for (int s = 0; s < 4; ++s) k[s] = (s < n_int && w.hit[s]) ? ((__float_as_uint(w.tmin[s]) & ~3u) | s) : ~0u;
         cas(k[0], k[1]); cas(k[2], k[3]); cas(k[0], k[2]); cas(k[1], k[3]); cas(k[1], k[2]);
         auto store = [&](int at, uint32_t v) {
-            if (at < P.stack_lds) stk[at * 64 + lane] = v;
+            if (at < P.stack_lds) stk[at * 64 + lane_fresh()] = v;
             else if (at < P.stack_cap) *ovf_slot(P, at, pix, n_pix) = v;
             else atomicOr(P.err, 2u);        // host stack bound violated: report, drop the entry
         };
@@ -778,7 +790,7 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
             }
         } else if (sp > 0) {
             const int at = sp - 1;
-            const uint32_t top = at < P.stack_lds ? stk[at * 64 + lane]
+            const uint32_t top = at < P.stack_lds ? stk[at * 64 + lane_fresh()]
                                                   : (at < P.stack_cap ? *ovf_slot(P, at, pix, n_pix) : 0u);
             const uint32_t rest = (top >> 6) & 3;
             node = (int)(top >> 8) + (int)((top >> 4) & 3);
@@ -814,7 +826,11 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
     if (leaf_n > 0) {
         L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first));
         L.prefix[lane] = pfx;
-        L.key[lane] = ~0ull;
+        // the empty key, materialised here: as a plain constant the register allocator keeps ~0ull live across
+        // the loop and spills it (a scratch reload and a vmcnt(0) wait on every leaf step)
+        uint32_t ones;
+        __asm__ volatile("v_mov_b32 %0, -1" : "=v"(ones));
+        L.key[lane] = ((unsigned long long)ones << 32) | ones;
     }
     uint32_t carry = 0;   // owner + 1 of the last pair of the previous round
     for (int base = 0; base < total; base += 64) {
@@ -1058,6 +1074,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     C.fw = (float)P.width;
     C.fh = (float)P.height;
     TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t wave_rays = 0;    // variant 8: rays of the wave (uniform); the other variants count per lane
 
     if (VARIANT == 0) {
         for (;;) {
@@ -1226,7 +1243,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     }
                     has_result = false;
                     if (live) {
-                        ++S.rays;
+                        if (!TILED) ++S.rays;
                         has_result = true;
                         node = 0;
                         sp = 0;
@@ -1247,6 +1264,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         if (COUNT) cnt.trace_calls++;
                     }
                 }
+                // variant 8 counts the wave's rays in a scalar (one VGPR less in the hot loop)
+                if (TILED) wave_rays += (uint32_t)__popcll(__ballot(parked && has_result));
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
             traverse_step4<COUNT>(P, S.o, S.d, inv, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
@@ -1322,7 +1341,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         P.sum[3 * (size_t)pix + 1] = S.pixel.y;
         P.sum[3 * (size_t)pix + 2] = S.pixel.z;
     }
-    const uint64_t wr = wave_sum_u64(S.rays);
+    const uint64_t wr = TILED ? (uint64_t)wave_rays : wave_sum_u64(S.rays);
     if (COUNT) {
         const uint64_t wb = wave_sum_u64(cnt.boxes), wt = wave_sum_u64(cnt.tris);
         const uint64_t ws = wave_sum_u64(cnt.spheres), wp = wave_sum_u64(S.paths);
