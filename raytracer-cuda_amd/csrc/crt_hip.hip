@@ -295,9 +295,16 @@ __device__ __forceinline__ float sphere_candidate(float4 f0, float4 f1, V3 o, V3
 
 // Any primitive of a CRT_BVH_REBUILT leaf: triangle, or sphere (record word 11 == 1; only when the tree
 // holds spheres — a uniform flag, so triangle-only trees skip the branch).
+// Record at a 32-bit byte offset from a uniform base: the load takes the SGPR base + VGPR offset form, no
+// 64-bit address arithmetic per lane (the host keeps primitive and 4-wide node arrays below 4 GiB).
+__device__ __forceinline__ const float4* rec_at(const float4* base, uint32_t byte_off) {
+    return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
 __device__ __forceinline__ float prim_test(const float4* __restrict__ prims, int p, V3 o, V3 d, float tmax, int& rank,
                                            bool tree_spheres = true) {
-    const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1], f2 = prims[3 * p + 2];
+    const float4* r = rec_at(prims, (uint32_t)p * 48u);
+    const float4 f0 = r[0], f1 = r[1], f2 = r[2];
     rank = __float_as_int(f2.z);
     if (tree_spheres && __float_as_int(f2.w) == 1) return sphere_candidate(f0, f1, o, d, tmax);
     return tri_test_rec(f0, f1, f2, o, d, tmax);
@@ -744,7 +751,7 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
     leaf_n = 0;
     leaf_first = 0;
     if (node >= 0) {
-        const float4* q = P.nodes + 8 * (size_t)node;
+        const float4* q = rec_at(P.nodes, (uint32_t)node << 7);
         const float4 mf = q[6];
         // keep the whole link row in the node's loads: left to itself the compiler loads leaf_first / counts
         // only inside the leaf branch, one more dependent load on a leaf step's critical path

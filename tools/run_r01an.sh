@@ -1,0 +1,11 @@
+# A/B: 32-bit byte offsets (SGPR base + VGPR offset loads) for 4-wide nodes and primitive records (default lib) vs the previous commit (lib_exp/prev)
+OUT=gpurun_out/r01an
+mkdir -p $OUT
+set -e
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_rebuilt.py tests/test_gpu_primitives.py tests/test_gpu_bvh_build.py -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+for rep in 1 2; do
+  CRT_HIP_LIB=raytracer-cuda_amd/lib_exp/prev/libcrt_hip.so timeout -k 10 300 python3 tools/bvh_eval.py --no-compare --spp 2000 --reps 1 --configs w4:l4:t2:T44:V8:o6 > $OUT/eval_prev_$rep.log 2>&1
+  timeout -k 10 300 python3 tools/bvh_eval.py --no-compare --spp 2000 --reps 1 --configs w4:l4:t2:T44:V8:o6 > $OUT/eval_new_$rep.log 2>&1
+done
+for f in $OUT/eval_*.log; do echo "$f $(grep -o '"kernel_ms": [0-9.]*' $f | tail -1) $(grep -o '"pixels_bit_equal": [0-9.]*' $f | tail -1)"; done > $OUT/summary.txt
+echo done
