@@ -753,10 +753,12 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
     if (node >= 0) {
         const float4* q = rec_at(P.nodes, (uint32_t)node << 7);
         const float4 mf = q[6];
-        // keep the whole link row in the node's loads: left to itself the compiler loads leaf_first / counts
-        // only inside the leaf branch, one more dependent load on a leaf step's critical path
-        __asm__ volatile("" : : "v"(mf.z), "v"(mf.w));
         const Wide4 w = wide_boxes(q, o, inv, closest);
+        // keep the whole link row in the node's loads: left to itself the compiler loads leaf_first / counts
+        // only inside the leaf branch, one more dependent load on a leaf step's critical path.  Pinned after the
+        // box tests, so the wait it implies is the one the boxes need anyway (pinned before them, it made the six
+        // box loads wait for the link row's round trip)
+        __asm__ volatile("" : : "v"(mf.z), "v"(mf.w));
         const int first_child = __float_as_int(mf.x);
         const int meta = __float_as_int(mf.y);
         const uint32_t counts = __float_as_uint(mf.w);
@@ -1237,6 +1239,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 if (COUNT) cnt.passes++;
                 if (parked) {
                     const uint64_t s0 = COUNT ? shader_clock() : 0;
+                    // (loading the shading record before this sphere test, to overlap its latency, measured +0.7 %:
+                    // profiles/r01ar)
                     if (CRT_SPHERES_LATE && has_result)
                         ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
                                           inv, closest, hit, sph_lds);
