@@ -541,17 +541,52 @@ struct Wide4 {
     bool hit[4];
 };
 
-// Slab test of the four child boxes against [0.001, tmax]; (lo - o) * inv in packed f32 (IEEE per half).
+// Slab test of the four child boxes against [0.001, tmax] in packed f32.  Default: lo * inv - o * inv as one
+// v_pk_fma_f32 per pair of planes (half the VALU of (lo - o) * inv).  Its error, about ulp(o) * |inv| in t, is
+// of the same order as that of (lo - o) * inv and far inside the boxes' 1e-5 * max(1, |coord|) padding
+// (DESIGN.md §2b).  inv must be finite: callers pass box_inv(1/d) (an infinite inv would make lo * inv - o * inv
+// inf - inf = NaN on one plane, and the min/max would then cull a box the ray runs inside of).
+// -DCRT_BOX_SUB_MUL restores (lo - o) * inv (A/B builds).
+// The traversal's 1/d: the exact 1/d clamped to +-2^100, so both planes keep their signs and magnitudes
+// (>= padding * 2^100) far above the rounding.  Identity in CRT_BOX_SUB_MUL builds.
+__device__ __forceinline__ V3 box_inv(V3 inv) {
+#ifdef CRT_BOX_SUB_MUL
+    return inv;
+#else
+    return v3(__builtin_amdgcn_fmed3f(inv.x, -0x1p100f, 0x1p100f), __builtin_amdgcn_fmed3f(inv.y, -0x1p100f, 0x1p100f),
+              __builtin_amdgcn_fmed3f(inv.z, -0x1p100f, 0x1p100f));
+#endif
+}
+// The per-ray spheres' exact 1/d (their reference box test) from the traversal's box_inv: recomputed only when a
+// component was clamped.
+__device__ __forceinline__ V3 sphere_inv(V3 d, V3 binv) {
+#ifndef CRT_BOX_SUB_MUL
+    if (fabsf(binv.x) == 0x1p100f || fabsf(binv.y) == 0x1p100f || fabsf(binv.z) == 0x1p100f)
+        return v3(recip_exact_any(d.x), recip_exact_any(d.y), recip_exact_any(d.z));
+#endif
+    return binv;
+}
 __device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ q, V3 o, V3 inv, float tmax) {
     const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
-    const pf2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
     const pf2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+#ifdef CRT_BOX_SUB_MUL
+    const pf2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
     const pf2 ax0 = ((pf2){lx.x, lx.y} - ox) * ix, ax1 = ((pf2){lx.z, lx.w} - ox) * ix;
     const pf2 bx0 = ((pf2){hx.x, hx.y} - ox) * ix, bx1 = ((pf2){hx.z, hx.w} - ox) * ix;
     const pf2 ay0 = ((pf2){ly.x, ly.y} - oy) * iy, ay1 = ((pf2){ly.z, ly.w} - oy) * iy;
     const pf2 by0 = ((pf2){hy.x, hy.y} - oy) * iy, by1 = ((pf2){hy.z, hy.w} - oy) * iy;
     const pf2 az0 = ((pf2){lz.x, lz.y} - oz) * iz, az1 = ((pf2){lz.z, lz.w} - oz) * iz;
     const pf2 bz0 = ((pf2){hz.x, hz.y} - oz) * iz, bz1 = ((pf2){hz.z, hz.w} - oz) * iz;
+#else
+    const float nx = -(o.x * inv.x), ny = -(o.y * inv.y), nz = -(o.z * inv.z);
+    const pf2 ox = {nx, nx}, oy = {ny, ny}, oz = {nz, nz};
+    const pf2 ax0 = __builtin_elementwise_fma((pf2){lx.x, lx.y}, ix, ox), ax1 = __builtin_elementwise_fma((pf2){lx.z, lx.w}, ix, ox);
+    const pf2 bx0 = __builtin_elementwise_fma((pf2){hx.x, hx.y}, ix, ox), bx1 = __builtin_elementwise_fma((pf2){hx.z, hx.w}, ix, ox);
+    const pf2 ay0 = __builtin_elementwise_fma((pf2){ly.x, ly.y}, iy, oy), ay1 = __builtin_elementwise_fma((pf2){ly.z, ly.w}, iy, oy);
+    const pf2 by0 = __builtin_elementwise_fma((pf2){hy.x, hy.y}, iy, oy), by1 = __builtin_elementwise_fma((pf2){hy.z, hy.w}, iy, oy);
+    const pf2 az0 = __builtin_elementwise_fma((pf2){lz.x, lz.y}, iz, oz), az1 = __builtin_elementwise_fma((pf2){lz.z, lz.w}, iz, oz);
+    const pf2 bz0 = __builtin_elementwise_fma((pf2){hz.x, hz.y}, iz, oz), bz1 = __builtin_elementwise_fma((pf2){hz.z, hz.w}, iz, oz);
+#endif
     const float ax[4] = {ax0.x, ax0.y, ax1.x, ax1.y}, bx[4] = {bx0.x, bx0.y, bx1.x, bx1.y};
     const float ay[4] = {ay0.x, ay0.y, ay1.x, ay1.y}, by[4] = {by0.x, by0.y, by1.x, by1.y};
     const float az[4] = {az0.x, az0.y, az1.x, az1.y}, bz[4] = {bz0.x, bz0.y, bz1.x, bz1.y};
@@ -690,7 +725,7 @@ __device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict
     int stack[64];
     while (node >= 0) {
         const float4* q = nodes + 8 * (size_t)node;
-        const Wide4 w = wide_boxes(q, o, inv, closest);
+        const Wide4 w = wide_boxes(q, o, box_inv(inv), closest);
         const float4 mf = q[6];
         const int first_child = __float_as_int(mf.x), n_int = __float_as_int(mf.y) & 0xff;
         const uint32_t counts = __float_as_uint(mf.w);
@@ -1126,7 +1161,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 if (parked) {
                     if (CRT_SPHERES_LATE && has_result)
                         ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
-                                          inv, closest, hit, sph_lds);
+                                          sphere_inv(S.d, inv), closest, hit, sph_lds);
                     if (has_result) shade(S, P, hit, closest);
                     live = next_ray(S, C, px, py, P.max_bounces);
                     has_result = false;
@@ -1209,6 +1244,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     if (!CRT_SPHERES_LATE)
                         ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d, inv,
                                     closest, hit, sph_lds);
+                    inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
                     if (COUNT) cnt.spheres += P.n_ray_spheres;
                     L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                     if (COUNT) cnt.trace_calls++;
@@ -1243,7 +1279,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     // profiles/r01ar)
                     if (CRT_SPHERES_LATE && has_result)
                         ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
-                                          inv, closest, hit, sph_lds);
+                                          sphere_inv(S.d, inv), closest, hit, sph_lds);
                     if (has_result) shade(S, P, hit, closest);
                     const uint64_t s1 = COUNT ? shader_clock() : 0;
                     live = next_ray(S, C, x, y, P.max_bounces);
@@ -1270,6 +1306,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         if (!CRT_SPHERES_LATE)
                             ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
                                         inv, closest, hit, sph_lds);
+                        inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
                         if (COUNT) cnt.spheres += P.n_ray_spheres;
                         L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                         if (COUNT) cnt.trace_calls++;
@@ -1492,6 +1529,7 @@ __global__ __launch_bounds__(256) void crt_wf_trace_kernel(WfParams W) {
             hit = -1;
             ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, o, d, inv, closest, hit,
                         sph_lds);
+            inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
             if (COUNT) cnt.spheres += P.n_ray_spheres;
             L.ray0[lane] = make_float4(o.x, o.y, o.z, d.x);
         }
