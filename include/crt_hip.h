@@ -215,33 +215,22 @@ int  crt_renderer_set_camera(crt_renderer* r, const crt_camera_desc* cam);
  * (CRT_BVH_REFERENCE, or REBUILT width 2; default 3): 0 = per-lane BVH traversal with per-lane leaf loops; 1 = per-lane
  * traversal with wave-cooperative leaf intersection; 2 = 1 + traversal-step scheduling with parked-lane regeneration
  * (lanes start their next ray without waiting for the wave's slowest trace); 3 = 2 + next-node prefetch overlapping
- * the leaf rounds; 4-8 run variant 3.  Scenes with 4-wide nodes (CRT_BVH_REBUILT, width 4): 4 = the variant-3
- * scheduling over 4-wide nodes with a per-lane stack, 16x16-pixel workgroups; 5 = the wavefront path (trace and shade
- * kernels over a queue of active pixels); 7 = 4 with a persistent grid whose lanes take pixels from a global queue
- * (no lane waits for its wave's slowest pixel); 8 = 4 with one wave per workgroup over 8x8 tiles in cost-probe order
- * (crt_renderer_set_schedule); 9 = 8 with K tiles per wave whose lanes take the wave's pixels in turn; anything
- * else = automatic: 8 when the render runs the cost probe (spp >= its
- * minimum), else 7. */
+ * the leaf rounds; 4, 7, 8 run variant 3.  Scenes with 4-wide nodes (CRT_BVH_REBUILT, width 4): 4 = the variant-3
+ * scheduling over 4-wide nodes with a per-lane stack, 16x16-pixel workgroups; 7 = 4 with a persistent grid whose lanes
+ * take pixels from a global queue (no lane waits for its wave's slowest pixel); 8 = 4 with one wave per workgroup over
+ * 8x8 tiles in cost-probe order (crt_renderer_set_schedule); anything else = automatic: 8 when the render runs the cost
+ * probe (spp >= its minimum), else 7.  Accepted values: 0-4, 7, 8. */
 int  crt_renderer_set_kernel_variant(crt_renderer* r, int variant);
-/* Variant 5: idle lanes that trigger a queue fetch in the trace kernel (1..64, default 16) and trace/shade
- * iterations between host reads of the queue length (default 16).  Variant-5 renders return after the
- * frame's kernels have been enqueued AND the queue has drained (host-synchronous). */
-int  crt_renderer_set_wavefront(crt_renderer* r, int refill_lanes, int check_iterations);
-long long crt_renderer_wavefront_iterations(const crt_renderer* r);   /* iterations of the last variant-5 render */
 /* Work order of variants 7 and 8 (4-wide scenes).  Cost probe: before the render, variant 4 traces probe_spp samples
- * per pixel over the same RNG state without writing anything, and the per-pixel ray counts order the work
+ * per pixel over the same RNG state without writing anything, and the per-pixel work estimates order the work
  * most-expensive-first (variant 7: pixels handed to lanes from a global queue; variant 8: 8x8 tiles, one wave per
- * workgroup).  Renders with fewer than min_spp samples per pixel skip the probe.  flags: CRT_SCHEDULE_XCD_BANDS
- * (variant 8: each of the 8 XCDs renders one horizontal strip of the image), CRT_SCHEDULE_FIRST_BLOCK (variant 7:
- * a wave's first 64 pixels run without refills), in bits 8-15 the tiles per wave of variant 9 (default 2), in bits
- * 16-19 variant 8's tile key (0 = slowest pixel, 1 = slowest + mean pixel, 2 = 0 raised to 3/4 of the neighbours';
- * the renderer starts with 2, the measured best).
- * Default -1 (automatic: 4 probe samples for renders of >= 1000 spp, else 2), 64, 0; probe_spp 0 disables the
+ * workgroup).  Renders with fewer than min_spp samples per pixel skip the probe.  flags bits 16-19: variant 8's tile
+ * key (0 = slowest pixel, 1 = slowest + mean pixel, 2 = 0 raised to 3/4 of the neighbours'; the renderer starts with
+ * 2, the measured best); other bits are ignored.
+ * Default -1 (automatic: 4 probe samples for renders of >= 1000 spp, else 2), 64, 2 << 16; probe_spp 0 disables the
  * probe.  Results never depend on the order. */
-#define CRT_SCHEDULE_XCD_BANDS  1
-#define CRT_SCHEDULE_FIRST_BLOCK 2
 int  crt_renderer_set_schedule(crt_renderer* r, int probe_spp, int min_spp, int flags);
-/* Variants 2-4, 7-9: number of parked lanes (1..64) that triggers a shading/regeneration pass; default 24 for
+/* Variants 2-4, 7, 8: number of parked lanes (1..64) that triggers a shading/regeneration pass; default 24 for
  * variants 2/3 and 44 for the 4-wide variants (setting it sets both). */
 int  crt_renderer_set_regen_threshold(crt_renderer* r, int lanes);
 /* Variant 4: per-lane traversal-stack entries kept in LDS (1..16, default 16); deeper entries spill to a

@@ -212,10 +212,8 @@ class Renderer:
     def init_rand(self, seed: int = 41, subsequence_base: int = 0, stream=None):
         check(_lib.hip().crt_renderer_init_rand(self.h, int(seed), int(subsequence_base), stream), "init_rand")
 
-    def set_schedule(self, probe_spp: int = -1, min_spp: int = 64, xcd_bands: bool = False, first_block: bool = False,
-                     tiles_per_wave: int = 2, tile_key: int = 2):
-        flags = ((1 if xcd_bands else 0) | (2 if first_block else 0) | ((int(tiles_per_wave) & 0xff) << 8)
-                 | ((int(tile_key) & 0xf) << 16))
+    def set_schedule(self, probe_spp: int = -1, min_spp: int = 64, tile_key: int = 2):
+        flags = (int(tile_key) & 0xf) << 16
         check(_lib.hip().crt_renderer_set_schedule(self.h, int(probe_spp), int(min_spp), flags), "set_schedule")
 
     def set_kernel_variant(self, variant: int):
@@ -226,12 +224,6 @@ class Renderer:
 
     def set_regen_threshold(self, lanes: int):
         check(_lib.hip().crt_renderer_set_regen_threshold(self.h, int(lanes)), "set_regen_threshold")
-
-    def set_wavefront(self, refill_lanes: int = 16, check_iterations: int = 16):
-        check(_lib.hip().crt_renderer_set_wavefront(self.h, int(refill_lanes), int(check_iterations)), "set_wavefront")
-
-    def wavefront_iterations(self) -> int:
-        return int(_lib.hip().crt_renderer_wavefront_iterations(self.h))
 
     def set_stack_lds(self, entries: int):
         check(_lib.hip().crt_renderer_set_stack_lds(self.h, int(entries)), "set_stack_lds")

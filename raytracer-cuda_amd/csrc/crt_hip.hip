@@ -72,8 +72,6 @@ struct RenderParams {
     uint32_t* __restrict__ queue;         // next unclaimed slot
     int n_slots;
     int tiles_x;                          // variant 8: 8x8 tiles per row (order[] holds tile indices)
-    int first_block_exclusive;            // variant 7: a wave refills lanes only after its first 64 pixels are done
-    int tiles_per_wave;                   // variant 9: 8x8 tiles in a wave's local pixel list
     uint32_t* __restrict__ probe_cost;    // probe launch (variant 4): rays per pixel; nothing else is written
 };
 
@@ -82,9 +80,6 @@ struct TraceCounts {
     // COUNT-mode section profile (variant 4; wave-uniform shader-clock cycles, s_memtime)
     uint64_t cyc_regen, cyc_step, cyc_round, passes;
     uint64_t cyc_shade, cyc_next;   // inside the regen pass: shade(), next_ray(); the rest is ray init
-#ifdef CRT_NODE_PREFETCH
-    float pf0 = 0.f, pf1 = 0.f;     // profiling build: one dword per cache line of the lane's next node
-#endif
 };
 __device__ __forceinline__ uint64_t shader_clock() { return __builtin_amdgcn_s_memtime(); }
 
@@ -252,39 +247,6 @@ struct WaveLds {
 // Möller–Trumbore (Mesh.cuh:266-308) on a triangle record; returns t or -1 when rejected (any accepted
 // t >= 0.001).
 typedef float pf2 __attribute__((ext_vector_type(2)));
-#ifdef CRT_TRI_PACKED
-// A/B variant (-DCRT_TRI_PACKED): the same Möller–Trumbore with its independent products paired into v_pk_mul_f32 /
-// v_pk_add_f32 (IEEE per half, no contraction), every expression in the reference's operation order, so the bits
-// are those of the scalar form below. Measured 3.8% slower on the headline frame (1578 vs 1521 ms render kernel,
-// same image): the pairing adds v_mov/v_perm shuffles and VGPRs on a path that is latency-, not ALU-bound.
-__device__ __forceinline__ float tri_test_rec(float4 f0, float4 f1, float4 f2, V3 o, V3 d, float tmax) {
-    const V3 e1 = v3(f0.w, f1.x, f1.y);
-    const V3 e2 = v3(f1.z, f1.w, f2.x);
-    // h = cross(d, e2): (d.y e2.z - d.z e2.y, d.z e2.x - d.x e2.z, d.x e2.y - d.y e2.x)
-    const pf2 hxy = (pf2){d.y, d.z} * (pf2){e2.z, e2.x} - (pf2){d.z, d.x} * (pf2){e2.y, e2.z};
-    const float hz = d.x * e2.y - d.y * e2.x;
-    const pf2 dp = (pf2){e1.x, e1.y} * hxy;
-    const float det = (dp.x + dp.y) + e1.z * hz;
-    if (fabsf(det) < 1e-8f) return -1.f;
-    const float f = recip_exact(det);          // == 1.f / det bit for bit (see crt_device.h)
-    const pf2 sxy = (pf2){o.x, o.y} - (pf2){f0.x, f0.y};
-    const float sz = o.z - f0.z;
-    const pf2 sp = sxy * hxy;
-    const float u = f * ((sp.x + sp.y) + sz * hz);
-    if (u < 0.f || u > 1.f) return -1.f;
-    // q = cross(s, e1): (s.y e1.z - s.z e1.y, s.z e1.x - s.x e1.z, s.x e1.y - s.y e1.x)
-    const pf2 qxy = (pf2){sxy.y, sz} * (pf2){e1.z, e1.x} - (pf2){sz, sxy.x} * (pf2){e1.y, e1.z};
-    const float qz = sxy.x * e1.y - sxy.y * e1.x;
-    // v = f * dot(d, q) and t = f * dot(e2, q), paired
-    const pf2 vt = (((pf2){d.x, e2.x} * (pf2){qxy.x, qxy.x} + (pf2){d.y, e2.y} * (pf2){qxy.y, qxy.y}) +
-                    (pf2){d.z, e2.z} * (pf2){qz, qz}) * (pf2){f, f};
-    const float v = vt.x;
-    if (v < 0.f || (u + v) > 1.f) return -1.f;
-    const float t = vt.y;
-    if (t < 0.001f || t > tmax) return -1.f;
-    return t;
-}
-#else
 __device__ __forceinline__ float tri_test_rec(float4 f0, float4 f1, float4 f2, V3 o, V3 d, float tmax) {
     const V3 e1 = v3(f0.w, f1.x, f1.y);
     const V3 e2 = v3(f1.z, f1.w, f2.x);
@@ -302,7 +264,6 @@ __device__ __forceinline__ float tri_test_rec(float4 f0, float4 f1, float4 f2, V
     if (t < 0.001f || t > tmax) return -1.f;
     return t;
 }
-#endif
 __device__ __forceinline__ float tri_test(const float4* __restrict__ prims, int p, V3 o, V3 d, float tmax, int& rank) {
     const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1], f2 = prims[3 * p + 2];
     rank = __float_as_int(f2.z);
@@ -569,50 +530,35 @@ __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, 
 // have a zero-thickness box far away (never hit).
 constexpr int STACK_LDS = 16;   // per-lane traversal-stack entries kept in LDS; deeper entries go to P.ovf
 
-typedef float pf2 __attribute__((ext_vector_type(2)));
-
 struct Wide4 {
     float tmin[4];
     bool hit[4];
 };
 
-// Slab test of the four child boxes against [0.001, tmax] in packed f32.  Default: lo * inv - o * inv as one
-// v_pk_fma_f32 per pair of planes (half the VALU of (lo - o) * inv).  Its error, about ulp(o) * |inv| in t, is
-// of the same order as that of (lo - o) * inv and far inside the boxes' 1e-5 * max(1, |coord|) padding
-// (DESIGN.md §2b).  inv must be finite: callers pass box_inv(1/d) (an infinite inv would make lo * inv - o * inv
-// inf - inf = NaN on one plane, and the min/max would then cull a box the ray runs inside of).
-// -DCRT_BOX_SUB_MUL restores (lo - o) * inv (A/B builds).
-// The traversal's 1/d: the exact 1/d clamped to +-2^100, so both planes keep their signs and magnitudes
-// (>= padding * 2^100) far above the rounding.  Identity in CRT_BOX_SUB_MUL builds.
+// Slab test of the four child boxes against [0.001, tmax] in packed f32: lo * inv - o * inv as one v_pk_fma_f32 per
+// pair of planes (half the VALU of (lo - o) * inv; measured -2.1 %, profiles/r01at).  Its error, about ulp(o) * |inv|
+// in t, is of the same order as that of (lo - o) * inv and far inside the boxes' 1e-5 * max(1, |coord|) padding
+// (DESIGN.md §2b).  inv must be finite AND o * inv / lo * inv must not overflow: an infinite product makes
+// lo * inv - o * inv = inf - inf = NaN on a plane, and the min/max would then cull a box the ray runs inside of.
+// The traversal's 1/d is therefore the exact 1/d clamped to +-2^64 (box_inv): a plane keeps its sign and a magnitude
+// >= padding * 2^64, far above the rounding, and |coord| * 2^64 stays finite for every |coord| < 2^60, the bound
+// crt_scene_create_ex enforces on the rebuilt tree's boxes and render() on the camera origin.
+constexpr float BOX_INV_CLAMP = 0x1p64f;
 __device__ __forceinline__ V3 box_inv(V3 inv) {
-#ifdef CRT_BOX_SUB_MUL
-    return inv;
-#else
-    return v3(__builtin_amdgcn_fmed3f(inv.x, -0x1p100f, 0x1p100f), __builtin_amdgcn_fmed3f(inv.y, -0x1p100f, 0x1p100f),
-              __builtin_amdgcn_fmed3f(inv.z, -0x1p100f, 0x1p100f));
-#endif
+    return v3(__builtin_amdgcn_fmed3f(inv.x, -BOX_INV_CLAMP, BOX_INV_CLAMP),
+              __builtin_amdgcn_fmed3f(inv.y, -BOX_INV_CLAMP, BOX_INV_CLAMP),
+              __builtin_amdgcn_fmed3f(inv.z, -BOX_INV_CLAMP, BOX_INV_CLAMP));
 }
 // The per-ray spheres' exact 1/d (their reference box test) from the traversal's box_inv: recomputed only when a
 // component was clamped.
 __device__ __forceinline__ V3 sphere_inv(V3 d, V3 binv) {
-#ifndef CRT_BOX_SUB_MUL
-    if (fabsf(binv.x) == 0x1p100f || fabsf(binv.y) == 0x1p100f || fabsf(binv.z) == 0x1p100f)
+    if (fabsf(binv.x) == BOX_INV_CLAMP || fabsf(binv.y) == BOX_INV_CLAMP || fabsf(binv.z) == BOX_INV_CLAMP)
         return v3(recip_exact_any(d.x), recip_exact_any(d.y), recip_exact_any(d.z));
-#endif
     return binv;
 }
 __device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ q, V3 o, V3 inv, float tmax) {
     const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
     const pf2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
-#ifdef CRT_BOX_SUB_MUL
-    const pf2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
-    const pf2 ax0 = ((pf2){lx.x, lx.y} - ox) * ix, ax1 = ((pf2){lx.z, lx.w} - ox) * ix;
-    const pf2 bx0 = ((pf2){hx.x, hx.y} - ox) * ix, bx1 = ((pf2){hx.z, hx.w} - ox) * ix;
-    const pf2 ay0 = ((pf2){ly.x, ly.y} - oy) * iy, ay1 = ((pf2){ly.z, ly.w} - oy) * iy;
-    const pf2 by0 = ((pf2){hy.x, hy.y} - oy) * iy, by1 = ((pf2){hy.z, hy.w} - oy) * iy;
-    const pf2 az0 = ((pf2){lz.x, lz.y} - oz) * iz, az1 = ((pf2){lz.z, lz.w} - oz) * iz;
-    const pf2 bz0 = ((pf2){hz.x, hz.y} - oz) * iz, bz1 = ((pf2){hz.z, hz.w} - oz) * iz;
-#else
     const float nx = -(o.x * inv.x), ny = -(o.y * inv.y), nz = -(o.z * inv.z);
     const pf2 ox = {nx, nx}, oy = {ny, ny}, oz = {nz, nz};
     const pf2 ax0 = __builtin_elementwise_fma((pf2){lx.x, lx.y}, ix, ox), ax1 = __builtin_elementwise_fma((pf2){lx.z, lx.w}, ix, ox);
@@ -621,7 +567,6 @@ __device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ q, V3 o, 
     const pf2 by0 = __builtin_elementwise_fma((pf2){hy.x, hy.y}, iy, oy), by1 = __builtin_elementwise_fma((pf2){hy.z, hy.w}, iy, oy);
     const pf2 az0 = __builtin_elementwise_fma((pf2){lz.x, lz.y}, iz, oz), az1 = __builtin_elementwise_fma((pf2){lz.z, lz.w}, iz, oz);
     const pf2 bz0 = __builtin_elementwise_fma((pf2){hz.x, hz.y}, iz, oz), bz1 = __builtin_elementwise_fma((pf2){hz.z, hz.w}, iz, oz);
-#endif
     const float ax[4] = {ax0.x, ax0.y, ax1.x, ax1.y}, bx[4] = {bx0.x, bx0.y, bx1.x, bx1.y};
     const float ay[4] = {ay0.x, ay0.y, ay1.x, ay1.y}, by[4] = {by0.x, by0.y, by1.x, by1.y};
     const float az[4] = {az0.x, az0.y, az1.x, az1.y}, bz[4] = {bz0.x, bz0.y, bz1.x, bz1.y};
@@ -669,12 +614,7 @@ __device__ __forceinline__ float sphere_root(float qa, float hb, float disc) {
 // provably beyond that hit then skips the correctly rounded sqrt and division: with su >= sqrtf(disc) (raw
 // v_sqrt_f32 is within 1 ulp, so 4 ulp of margin), fl(-hb - su) <= fl(-hb - sqrtf(disc)) by monotone rounding, and
 // fl(-hb - su) > fl(closest * qa) * (1 + 1e-5) puts the exact root above nextafter(closest).  The far root is
-// larger still.  -DCRT_RAY_SPHERES_FIRST restores the test at ray start (A/B builds).
-#ifdef CRT_RAY_SPHERES_FIRST
-#define CRT_SPHERES_LATE 0
-#else
-#define CRT_SPHERES_LATE 1
-#endif
+// larger still.  (Testing them at ray start instead measured +2.1 %, profiles/r01ag.)
 __device__ __forceinline__ bool sphere_beyond(float qa, float hb, float disc, float closest) {
     if (!(disc > 1e-30f) || !(closest < __builtin_inff())) return false;
     const float su = __builtin_amdgcn_sqrtf(disc) * (1.0f + 0x1p-21f);
@@ -722,9 +662,6 @@ __device__ __forceinline__ void ray_spheres(const float4* __restrict__ prims, co
                                             int n_chain, int first, int n, V3 o, V3 d, V3 inv, float& closest,
                                             int& hit, const float* sph2 = nullptr) {
     if (n == 0) return;
-#ifdef CRT_PROFILE_NO_RAY_SPHERES
-    return;   // profiling build only (tools/build_profile_lib.sh): measures what the per-ray sphere tests cost
-#endif
     if (n == 2 && sph2) {
         ray_spheres2<LATE>(sph2, sph2 + 12, o, d, inv, closest, hit);
         return;
@@ -879,13 +816,6 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
             node = -1;
         }
     }
-#ifdef CRT_NODE_PREFETCH
-    if (node >= 0) {   // touch the next node's two 64 B lines now; the value is never waited on in the loop
-        const float* a = reinterpret_cast<const float*>(P.nodes + 8 * (size_t)node);
-        cnt.pf0 = a[0];
-        cnt.pf1 = a[16];
-    }
-#endif
 }
 
 template <bool COUNT>
@@ -1090,7 +1020,7 @@ __device__ unsigned long long g_wave_prof[2 * 4 * 65536];
 
 // Waves per workgroup: 4 (16x16 pixels), or 1 for variant 8 (one 8x8 tile per workgroup, so a finished wave frees
 // its slot at once instead of holding it until its three siblings end).
-template <int VARIANT> struct KernelShape { static constexpr int waves = (VARIANT == 8 || VARIANT == 9) ? 1 : 4; };
+template <int VARIANT> struct KernelShape { static constexpr int waves = VARIANT == 8 ? 1 : 4; };
 
 template <bool COUNT, int VARIANT, int MINW>
 __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_render_kernel(RenderParams P) {
@@ -1100,11 +1030,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     constexpr int WGW = KernelShape<VARIANT>::waves;
     __shared__ WaveLds lds[VARIANT >= 1 ? WGW : 1];
     // variant 4: 16 LDS stack entries per lane at 5 waves/SIMD; 12 at 6+ so 6 workgroups fit the 160 KiB
-    // variant 9: variant 7's lane refill from a wave-local list instead of the global queue: workgroup b (one wave)
-    // owns tiles order[b*K .. b*K+K-1] (K = P.tiles_per_wave, tiles most expensive first) and its lanes take their
-    // pixels in turn
-    constexpr bool LOCALQ = VARIANT == 9;
-    constexpr bool PERSIST = VARIANT == 7 || LOCALQ;
+    constexpr bool PERSIST = VARIANT == 7;
     constexpr bool TILED = VARIANT == 8;    // variant 4 with one wave per workgroup and a tile order
     constexpr bool WIDE = VARIANT == 4 || PERSIST || TILED;
     constexpr int SD = WIDE ? (MINW >= 7 ? 11 : MINW >= 6 ? 12 : STACK_LDS) : 1;
@@ -1120,7 +1046,6 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     int x, y;
     if (TILED) {                               // workgroup b renders 8x8 tile order[b]
         const uint32_t t = P.order ? P.order[blockIdx.x] : blockIdx.x;
-        if (t == 0xffffffffu) return;          // padding slot of the XCD-band order
         x = (int)(t % (uint32_t)P.tiles_x) * 8 + (lane & 7);
         y = (int)(t / (uint32_t)P.tiles_x) * 8 + (lane >> 3);
     } else {
@@ -1173,8 +1098,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         uint32_t* stk = stack_lds + wave * SD * 64;
         const float INF = __builtin_inff();
         const size_t n_pix = (size_t)P.width * P.height;
-        const uint32_t total_slots = LOCALQ ? (blockIdx.x + 1u) * (uint32_t)P.tiles_per_wave * 64u : (uint32_t)P.n_slots;
-        uint32_t next_block = blockIdx.x * (uint32_t)P.tiles_per_wave * 64u;   // LOCALQ: the wave's next tile
+        const uint32_t total_slots = (uint32_t)P.n_slots;
         const uint64_t below = (1ull << lane) - 1ull;
         bool live = false, has_result = false, have = false;
         int node = -1, sp = 0, hit = -1, px = 0, py = 0, ppix = 0;
@@ -1182,9 +1106,6 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         V3 inv = v3(0.f, 0.f, 0.f);
         uint32_t pool = 0, used = 64;    // wave-uniform: first slot of the reserved block, slots handed out
         bool exhausted = false;
-        // first_block_exclusive: the wave's first 64 pixels (the most expensive, in probe order) run without
-        // refills, so their slow lanes end in an emptying wave (variant 4's behaviour); afterwards lanes refill
-        int fb = P.first_block_exclusive ? 0 : 2;   // 0: nothing assigned yet, 1: first block running, 2: refill
         L.owner_at[lane] = 0;
         for (;;) {
             const bool parked = live && node < 0;
@@ -1194,7 +1115,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             if (n_parked >= P.regen_threshold || n_parked == n_live) {
                 if (COUNT) cnt.passes++;
                 if (parked) {
-                    if (CRT_SPHERES_LATE && has_result)
+                    if (has_result)
                         ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
                                           sphere_inv(S.d, inv), closest, hit, sph_lds);
                     if (has_result) shade(S, P, hit, closest);
@@ -1209,35 +1130,20 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     P.sum[3 * (size_t)ppix + 2] = S.pixel.z;
                     have = false;
                 }
-                if (fb == 1 && !__ballot(have)) fb = 2;   // the first block is done: refill from now on
-                while (!exhausted && fb != 1) {     // lanes without a pixel take the next slots
+                while (!exhausted) {                // lanes without a pixel take the next slots
                     const uint64_t need = __ballot(!have);
                     if (need == 0) break;
                     if (used >= 64u) {
-                        if (LOCALQ) {
-                            pool = next_block;
-                            next_block += 64u;
-                        } else {
-                            uint32_t b = 0;
-                            if (lane == 0) b = atomicAdd(P.queue, 64u);
-                            pool = __builtin_amdgcn_readfirstlane(b);
-                        }
+                        uint32_t b = 0;
+                        if (lane == 0) b = atomicAdd(P.queue, 64u);
+                        pool = __builtin_amdgcn_readfirstlane(b);
                         used = 0;
                         if (pool >= total_slots) { exhausted = true; break; }
                     }
                     const uint32_t take = min((uint32_t)__popcll(need), 64u - used);
                     const uint32_t rank = (uint32_t)__popcll(need & below);
                     if (!have && rank < take && pool + used + rank < total_slots) {
-                        uint32_t pixel;
-                        if (LOCALQ) {                 // slot -> (tile order[slot / 64], pixel slot % 64 of it)
-                            const uint32_t slot = pool + used + rank, tile = P.order[slot >> 6], q = slot & 63u;
-                            const int tx = (int)(tile % (uint32_t)P.tiles_x) * 8 + (int)(q & 7u);
-                            const int ty = (int)(tile / (uint32_t)P.tiles_x) * 8 + (int)(q >> 3);
-                            pixel = (tile != 0xffffffffu && tx < P.width && ty < P.height) ? (uint32_t)(ty * P.width + tx)
-                                                                                          : 0xffffffffu;
-                        } else {
-                            pixel = P.order[pool + used + rank];
-                        }
+                        const uint32_t pixel = P.order[pool + used + rank];
                         if (pixel != 0xffffffffu) {
                             ppix = (int)pixel;
                             px = ppix % P.width;
@@ -1263,7 +1169,6 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     }
                     used += take;
                 }
-                if (fb == 0) fb = 1;
                 if (live && node < 0) {          // a new ray: the parked lanes' next ray or a new pixel's first
                     ++S.rays;
                     has_result = true;
@@ -1271,14 +1176,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     sp = 0;
                     closest = INF;
                     hit = -1;
-#ifdef CRT_INV_IEEE
-                    inv = v3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
-#else
                     inv = v3(recip_exact_any(S.d.x), recip_exact_any(S.d.y), recip_exact_any(S.d.z));
-#endif
-                    if (!CRT_SPHERES_LATE)
-                        ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d, inv,
-                                    closest, hit, sph_lds);
                     inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
                     if (COUNT) cnt.spheres += P.n_ray_spheres;
                     L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
@@ -1312,7 +1210,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     const uint64_t s0 = COUNT ? shader_clock() : 0;
                     // (loading the shading record before this sphere test, to overlap its latency, measured +0.7 %:
                     // profiles/r01ar)
-                    if (CRT_SPHERES_LATE && has_result)
+                    if (has_result)
                         ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
                                           sphere_inv(S.d, inv), closest, hit, sph_lds);
                     if (has_result) shade(S, P, hit, closest);
@@ -1333,14 +1231,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         hit = -1;
                         // exact 1/d: the per-ray spheres' reference box tests need it (the padded traversal
                         // would do with rcp)
-#ifdef CRT_INV_IEEE
-                        inv = v3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
-#else
                         inv = v3(recip_exact_any(S.d.x), recip_exact_any(S.d.y), recip_exact_any(S.d.z));
-#endif
-                        if (!CRT_SPHERES_LATE)
-                            ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
-                                        inv, closest, hit, sph_lds);
                         inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
                         if (COUNT) cnt.spheres += P.n_ray_spheres;
                         L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
@@ -1456,251 +1347,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         }
     }
 #endif
-#ifdef CRT_NODE_PREFETCH
-    if (cnt.pf0 == 1.5e-38f && cnt.pf1 == -1.5e-38f) atomicOr(P.err, 0u);   // keeps the prefetch loads
-#endif
 }
 
-// ------------------------------------------------------------------ wavefront path (variant 5)
-// Trace and shade as separate kernels over a queue of active pixels (4-wide BVH scenes).  Each pixel has
-// at most one path in flight and its samples stay in order, so every pixel's RNG stream and sum evolve
-// exactly as in the megakernels.  Per-pixel state lives in HBM between the phases:
-//   ray[2p], ray[2p+1] = (o.xyz, d.x), (d.y, d.z, t, hit rank)   path[p] = (thr.xyz, bounce)
-//   remaining[p] = samples not started; rng / sum as for the megakernels.
-struct WfParams {
-    RenderParams P;
-    float4* __restrict__ ray;
-    float4* __restrict__ path;
-    int* __restrict__ remaining;
-    const int* __restrict__ queue_in;
-    int* __restrict__ queue_out;
-    const int* __restrict__ count_in;
-    int* __restrict__ count_out;
-    int* __restrict__ head;      // trace: queue fetch cursor
-    int initial;                 // shade: first pass of the launch (no hit to shade)
-    int refill;                  // trace: idle lanes that trigger a queue fetch
-};
-
-constexpr int WF_STACK = 16;     // trace kernel: per-lane stack entries in LDS (deeper ones in P.ovf)
-
-__device__ __forceinline__ CamRegs cam_regs(const RenderParams& P) {
-    const crt_camera_desc& Cd = P.cam;
-    CamRegs C;
-    C.pos = v3(Cd.origin[0], Cd.origin[1], Cd.origin[2]);
-    C.llc = v3(Cd.lower_left[0], Cd.lower_left[1], Cd.lower_left[2]);
-    C.hor = v3(Cd.horizontal[0], Cd.horizontal[1], Cd.horizontal[2]);
-    C.ver = v3(Cd.vertical[0], Cd.vertical[1], Cd.vertical[2]);
-    C.right = v3(Cd.right[0], Cd.right[1], Cd.right[2]);
-    C.up = v3(Cd.up[0], Cd.up[1], Cd.up[2]);
-    C.lens = Cd.lens_radius;
-    C.fw = (float)P.width;
-    C.fh = (float)P.height;
-    return C;
-}
-
-// Streaming per-pixel state: non-temporal so it does not push the scene out of L2.
-template <typename T> __device__ __forceinline__ T ld_nt(const T* p) { return __builtin_nontemporal_load(p); }
-template <typename T> __device__ __forceinline__ void st_nt(T v, T* p) { __builtin_nontemporal_store(v, p); }
-typedef float nf4 __attribute__((ext_vector_type(4)));
-typedef float nf2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float4 ld_nt(const float4* p) {
-    const nf4 v = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void st_nt(float4 v, float4* p) {
-    const nf4 n = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(n, reinterpret_cast<nf4*>(p));
-}
-__device__ __forceinline__ void st_nt(float2 v, float2* p) {
-    const nf2 n = {v.x, v.y};
-    __builtin_nontemporal_store(n, reinterpret_cast<nf2*>(p));
-}
-
-constexpr int WF_CHUNK = 256;    // queue entries a trace wave claims per global atomic
-
-// Trace phase: persistent waves over the queue.  Each wave claims chunks of WF_CHUNK queue entries with one
-// atomic and feeds its lanes from the chunk; every lane keeps a two-stage prefetch (queue entry, then the
-// ray) so a lane whose trace ends swaps in an already-loaded ray at the next step.  The variant-4 step runs
-// on every wave iteration, so traversal steps stay full until the queue drains.
-template <bool COUNT>
-__global__ __launch_bounds__(256) void crt_wf_trace_kernel(WfParams W) {
-    const RenderParams& P = W.P;
-    __shared__ WaveLds lds[4];
-    __shared__ uint32_t stack_lds[4 * WF_STACK * 64];
-    __shared__ float sph_lds[24];
-    if (threadIdx.x < 24) sph_lds[threadIdx.x] = (&P.sph2[0][0])[threadIdx.x];
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    WaveLds& L = lds[wave];
-    uint32_t* stk = stack_lds + wave * WF_STACK * 64;
-    const int count = *W.count_in;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        *W.count_out = 0;                                  // the shade phase appends to it next
-        atomicAdd(&P.counters[0], (unsigned long long)count);   // every queued pixel traces one ray
-    }
-    const size_t n_pix = (size_t)P.width * P.height;
-    const float INF = __builtin_inff();
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
-    int p = -1, node = -1, sp = 0, hit = -1;
-    float closest = INF;
-    V3 o = v3(0.f, 0.f, 0.f), d = o, inv = o;
-    int nq = -1, np = -1;                                  // prefetch: queue entry loaded / ray loaded
-    float4 r0n = make_float4(0.f, 0.f, 0.f, 0.f), r1n = r0n;
-    int chunk_next = 0, chunk_end = 0;                     // wave-uniform
-    bool more = true;                                      // wave-uniform: the global queue may have entries
-    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    L.owner_at[lane] = 0;      // traverse_step4: owner + 1, 0 = none
-    for (;;) {
-        if (p < 0 && np >= 0) {                            // swap in the prefetched ray
-            p = np;
-            np = -1;
-            o = v3(r0n.x, r0n.y, r0n.z);
-            d = v3(r0n.w, r1n.x, r1n.y);
-            inv = v3(recip_exact_any(d.x), recip_exact_any(d.y), recip_exact_any(d.z));
-            node = 0;
-            sp = 0;
-            closest = INF;
-            hit = -1;
-            ray_spheres(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, o, d, inv, closest, hit,
-                        sph_lds);
-            inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
-            if (COUNT) cnt.spheres += P.n_ray_spheres;
-            L.ray0[lane] = make_float4(o.x, o.y, o.z, d.x);
-        }
-        if (np < 0 && nq >= 0) {                           // stage 2: start the ray loads
-            np = nq;
-            nq = -1;
-            r0n = ld_nt(&W.ray[2 * (size_t)np]);
-            r1n = ld_nt(&W.ray[2 * (size_t)np + 1]);
-        }
-        const uint64_t need = __ballot(nq < 0 && np < 0);  // stage 1: lanes with an empty pipeline
-        const int n_need = __popcll(need);
-        if (n_need >= W.refill || n_need == 64) {
-            if (chunk_next >= chunk_end && more) {
-                int b = count;
-                if (lane == 0 && __hip_atomic_load(W.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < count)
-                    b = atomicAdd(W.head, WF_CHUNK);   // (skip the contended atomic once the queue is claimed)
-                b = __shfl(b, 0);
-                chunk_next = b;
-                chunk_end = min(b + WF_CHUNK, count);
-                if (b + WF_CHUNK >= count) more = false;
-            }
-            const int take = min(max(chunk_end - chunk_next, 0), n_need);
-            const int rank = __popcll(need & lt_mask);
-            if (((need >> lane) & 1ull) && rank < take) nq = ld_nt(&W.queue_in[chunk_next + rank]);
-            chunk_next += take;
-        }
-        if (!__ballot(p >= 0 || np >= 0 || nq >= 0)) {
-            if (!more && chunk_next >= chunk_end) break;
-            continue;
-        }
-        traverse_step4<COUNT>(P, o, d, inv, node, sp, closest, hit, cnt, L, stk, lane, p < 0 ? 0 : (size_t)p, n_pix);
-        if (p >= 0 && node < 0) {
-            st_nt(make_float2(closest, __int_as_float(hit)), reinterpret_cast<float2*>(&W.ray[2 * (size_t)p + 1].z));
-            p = -1;
-        }
-    }
-    if (COUNT) {
-        const uint64_t wb = wave_sum_u64(cnt.boxes), wt = wave_sum_u64(cnt.tris), ws = wave_sum_u64(cnt.spheres);
-        if (lane == 0) {
-            atomicAdd(&P.counters[1], (unsigned long long)wb);
-            atomicAdd(&P.counters[2], (unsigned long long)wt);
-            atomicAdd(&P.counters[3], (unsigned long long)ws);
-            atomicAdd(&P.counters[5], 64ull * cnt.step_slots);
-            atomicAdd(&P.counters[6], 64ull * cnt.round_slots);
-            atomicAdd(&P.counters[9], (unsigned long long)cnt.cyc_step);
-            atomicAdd(&P.counters[10], (unsigned long long)cnt.cyc_round);
-        }
-    }
-}
-
-// Shade phase: one queued pixel per lane (block-stride loop, uniform trip count per workgroup): shade the
-// traced hit, start the pixel's next ray (next bounce, or next sample), append the pixel to the next queue
-// while it has a ray to trace (one atomic per workgroup and loop iteration).
-template <bool COUNT>
-__global__ __launch_bounds__(256) void crt_wf_shade_kernel(WfParams W) {
-    const RenderParams& P = W.P;
-    __shared__ int s_cnt[4];
-    __shared__ int s_base;
-    const int n_pix = P.width * P.height;
-    const int count = W.initial ? n_pix : *W.count_in;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *W.head = 0;         // fetch cursor of the next trace phase
-    const CamRegs C = cam_regs(P);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t paths = 0;
-    const uint64_t c0 = COUNT ? shader_clock() : 0;
-    for (int base = blockIdx.x * 256; base < count; base += gridDim.x * 256) {
-        const int i = base + (int)threadIdx.x;
-        bool live = false;
-        int p = -1;
-        if (i < count) {
-            p = W.initial ? i : ld_nt(&W.queue_in[i]);
-            const int x = p % P.width, y = p / P.width;
-            PathState S;
-            uint32_t* rw = P.rng + 6 * (size_t)p;
-            S.s = Rng{ld_nt(rw), ld_nt(rw + 1), ld_nt(rw + 2), ld_nt(rw + 3), ld_nt(rw + 4), ld_nt(rw + 5)};
-            S.rays = 0;
-            S.paths = 0;
-            float* sw = P.sum + 3 * (size_t)p;
-            if (W.initial) {
-                S.pixel = P.accumulate ? v3(ld_nt(sw), ld_nt(sw + 1), ld_nt(sw + 2)) : v3(0.f, 0.f, 0.f);
-                S.o = v3(0, 0, 0); S.d = v3(0, 0, 1); S.thr = v3(1, 1, 1);
-                S.bounce = 0;
-                S.remaining = P.spp;
-                S.need_new = true;
-                live = next_ray(S, C, x, y, P.max_bounces);
-            } else {
-                S.pixel = v3(ld_nt(sw), ld_nt(sw + 1), ld_nt(sw + 2));
-                const float4 r0 = ld_nt(&W.ray[2 * (size_t)p]), r1 = ld_nt(&W.ray[2 * (size_t)p + 1]);
-                const float4 pa = ld_nt(&W.path[p]);
-                S.o = v3(r0.x, r0.y, r0.z);
-                S.d = v3(r0.w, r1.x, r1.y);
-                S.thr = v3(pa.x, pa.y, pa.z);
-                S.bounce = __float_as_int(pa.w);
-                S.remaining = ld_nt(&W.remaining[p]);
-                S.need_new = false;
-                shade(S, P, __float_as_int(r1.w), r1.z);
-                live = next_ray(S, C, x, y, P.max_bounces);
-            }
-            st_nt(S.s.v0, rw); st_nt(S.s.v1, rw + 1); st_nt(S.s.v2, rw + 2);
-            st_nt(S.s.v3, rw + 3); st_nt(S.s.v4, rw + 4); st_nt(S.s.d, rw + 5);
-            st_nt(S.pixel.x, sw); st_nt(S.pixel.y, sw + 1); st_nt(S.pixel.z, sw + 2);
-            st_nt(S.remaining, &W.remaining[p]);
-            paths += S.paths;
-            if (live) {
-                st_nt(make_float4(S.o.x, S.o.y, S.o.z, S.d.x), &W.ray[2 * (size_t)p]);
-                st_nt(make_float4(S.d.y, S.d.z, 0.f, 0.f), &W.ray[2 * (size_t)p + 1]);
-                st_nt(make_float4(S.thr.x, S.thr.y, S.thr.z, __int_as_float(S.bounce)), &W.path[p]);
-            }
-        }
-        // append this workgroup's live pixels to the next queue with one atomic
-        const uint64_t m = __ballot(live);
-        if (lane == 0) s_cnt[wave] = __popcll(m);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const int tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-            s_base = tot ? atomicAdd(W.count_out, tot) : 0;
-        }
-        __syncthreads();
-        int off = s_base;
-        for (int w = 0; w < wave; ++w) off += s_cnt[w];
-        if (live) st_nt(p, &W.queue_out[off + __popcll(m & ((1ull << lane) - 1ull))]);
-        __syncthreads();
-    }
-    if (COUNT) {
-        const uint64_t wp = wave_sum_u64(paths);
-        if (lane == 0) {
-            atomicAdd(&P.counters[4], (unsigned long long)wp);
-            atomicAdd(&P.counters[8], (unsigned long long)(shader_clock() - c0));
-            atomicAdd(&P.counters[11], 1ull);
-        }
-    }
-}
-
-// Diagnostic: paths follow scene A (variant-0 trace); every ray is ALSO traced through scene B and the two
-// closest hits compared.  counters: [0] rays, [1] rays whose hit rank differs, [2] rays with the same
-// rank but a different t, [3] rays where B misses but A hits, [4] rays where A misses but B hits.
 struct CompareParams {
     RenderParams A;
     const float4* __restrict__ nodes_b;
@@ -2021,22 +1669,6 @@ __global__ void crt_tile_neighbour_kernel(const uint32_t* __restrict__ key_in, i
     key_out[t] = max(key_in[t], (nb * 3u) / 4u);
 }
 
-// Variant 8, XCD bands: workgroups are dealt round-robin over the 8 XCDs, so workgroup b runs on the XCD of
-// b % 8.  Band k (tiles [k*per, (k+1)*per) in row order, a horizontal strip of the image) goes to workgroups
-// b % 8 == k, in the order `sorted` holds it, so each XCD's L2 serves one strip.
-__global__ void crt_order_bands_kernel(const uint32_t* __restrict__ sorted, int n_tiles, int per,
-                                       uint32_t* __restrict__ order) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= 8 * per) return;
-    const int k = b % 8, j = b / 8, t = k * per + j;
-    order[b] = (j < per && t < n_tiles) ? (sorted ? sorted[t] : (uint32_t)t) : 0xffffffffu;
-}
-
-__global__ void crt_order_iota_kernel(uint32_t* __restrict__ order, int n) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < n) order[t] = (uint32_t)t;
-}
-
 // No probe: 8x8 tiles in row order, pixels row-major inside a tile (a wave's first 64 slots are one tile, so
 // its primary rays are coherent); slots of partial edge tiles hold ~0.
 __global__ void crt_order_tiles_kernel(uint32_t* __restrict__ order, int width, int height, int n_slots) {
@@ -2283,9 +1915,10 @@ struct Rebuilt {
             bool finite = true;
             for (int a = 0; a < 3; ++a) {
                 it.c[a] = 0.5f * it.lo[a] + 0.5f * it.hi[a];
-                finite = finite && std::isfinite(it.lo[a]) && std::isfinite(it.hi[a]);
+                // box_inv's clamp (2^64) keeps |coord| * inv finite only below 2^60 (wide_boxes)
+                finite = finite && std::fabs(it.lo[a]) < 0x1p60f && std::fabs(it.hi[a]) < 0x1p60f;
             }
-            if (!finite) { err = "non-finite primitive bounds"; return false; }
+            if (!finite) { err = "primitive bounds non-finite or beyond 2^60"; return false; }
             items.push_back(it);
         }
         rank_code.assign(F.rank_code.size(), 0);
@@ -2470,6 +2103,8 @@ struct crt_scene {
     long excluded = 0;
 };
 
+constexpr int ERR_WORD = 15;      // d_counters word of the device error flags (RenderParams::err)
+
 struct crt_renderer {
     int device = 0, width = 0, height = 0;
     uint32_t* d_rng = nullptr;
@@ -2495,11 +2130,7 @@ struct crt_renderer {
     int probe_spp = -1;            // samples per pixel of the cost probe; 0 = no probe (8x8-tile order),
                                    // -1 = automatic: 4 for renders of >= 1000 spp, else 2 (profiles/r01ad)
     int probe_min_spp = 64;        // renders with fewer samples per pixel skip the probe
-    int xcd_bands = 0;             // variant 8: each XCD renders one horizontal strip (see crt_order_bands_kernel)
-    int first_block_exclusive = 0; // variant 7: see RenderParams::first_block_exclusive
-    int tiles_per_wave = 2;        // variant 9
     int tile_key_mode = 2;         // variant 8: see crt_tile_cost_kernel (2: measured best, profiles/r01ac)
-    uint32_t* d_sorted = nullptr;  // variant 8: tiles sorted per band
     int n_cus = 0;
     int variant = 3;               // see crt_renderer_set_kernel_variant
     unsigned long long diag[3] = {0, 0, 0};
@@ -2511,16 +2142,6 @@ struct crt_renderer {
     size_t ovf_entries = 0;
     int stack_lds = STACK_LDS;     // variant 4: per-lane stack entries kept in LDS
     // variant 5 (wavefront) state, allocated on first use
-    float4* d_wf_ray = nullptr;
-    float4* d_wf_path = nullptr;
-    int* d_wf_rem = nullptr;
-    int* d_wf_queue = nullptr;     // 2 x W*H
-    int* d_wf_ctr = nullptr;       // count[0], count[1], head
-    int* h_wf_count = nullptr;     // pinned
-    int wf_refill = 16;
-    int wf_check = 16;             // iterations between host checks of the queue length
-    int n_cu = 0;
-    long long wf_iterations = 0;
 };
 
 namespace {
@@ -2810,13 +2431,6 @@ void crt_renderer_destroy(crt_renderer* R) {
     if (R->d_order_hist) (void)hipFree(R->d_order_hist);
     if (R->d_tile_key) (void)hipFree(R->d_tile_key);
     if (R->d_rng_cache) (void)hipFree(R->d_rng_cache);
-    if (R->d_sorted) (void)hipFree(R->d_sorted);
-    if (R->d_wf_ray) (void)hipFree(R->d_wf_ray);
-    if (R->d_wf_path) (void)hipFree(R->d_wf_path);
-    if (R->d_wf_rem) (void)hipFree(R->d_wf_rem);
-    if (R->d_wf_queue) (void)hipFree(R->d_wf_queue);
-    if (R->d_wf_ctr) (void)hipFree(R->d_wf_ctr);
-    if (R->h_wf_count) (void)hipHostFree(R->h_wf_count);
     if (R->ev0) (void)hipEventDestroy(R->ev0);
     if (R->ev1) (void)hipEventDestroy(R->ev1);
     delete R;
@@ -2853,7 +2467,8 @@ int crt_renderer_init_rand(crt_renderer* R, unsigned long long seed, unsigned lo
 }
 
 int crt_renderer_set_kernel_variant(crt_renderer* R, int variant) {
-    if (!R || variant < 0 || variant > 9 || variant == 6) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant");
+    if (!R || variant < 0 || variant > 8 || variant == 5 || variant == 6)
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant (0-4, 7, 8)");
     R->variant = variant;
     return CRT_OK;
 }
@@ -2862,9 +2477,6 @@ int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int f
     if (!R || probe_spp < -1 || probe_spp > 64 || min_spp < 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad schedule");
     R->probe_spp = probe_spp < 0 ? -1 : probe_spp;
     R->probe_min_spp = min_spp;
-    R->xcd_bands = (flags & 1) ? 1 : 0;
-    R->first_block_exclusive = (flags & 2) ? 1 : 0;
-    R->tiles_per_wave = ((flags >> 8) & 0xff) ? ((flags >> 8) & 0xff) : 2;
     R->tile_key_mode = (flags >> 16) & 0xf;   // 0 = slowest pixel (callers that pass 0 get the plain key)
     return CRT_OK;
 }
@@ -2895,84 +2507,6 @@ int crt_renderer_set_camera(crt_renderer* R, const crt_camera_desc* cam) {
     return CRT_OK;
 }
 
-// Variant 5 driver: initial shade pass (first ray of every pixel), then trace / shade pairs until the queue
-// is empty.  The queue length is read back every wf_check iterations (the only host synchronisation).
-static int render_wavefront(crt_renderer* R, RenderParams& P, bool cnt, hipStream_t st) {
-    const size_t n = (size_t)R->width * R->height;
-    if (!R->d_wf_ray) {
-        hipError_t e;
-        if ((e = hipMalloc((void**)&R->d_wf_ray, n * 32)) != hipSuccess ||
-            (e = hipMalloc((void**)&R->d_wf_path, n * 16)) != hipSuccess ||
-            (e = hipMalloc((void**)&R->d_wf_rem, n * 4)) != hipSuccess ||
-            (e = hipMalloc((void**)&R->d_wf_queue, 2 * n * 4)) != hipSuccess ||
-            (e = hipMalloc((void**)&R->d_wf_ctr, 4 * sizeof(int))) != hipSuccess ||
-            (e = hipHostMalloc((void**)&R->h_wf_count, sizeof(int))) != hipSuccess)
-            return set_error(CRT_ERR_HIP, std::string("wavefront buffers: ") + hipGetErrorString(e));
-        int dev_cu = 0;
-        HIP_TRY(hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, R->device));
-        R->n_cu = dev_cu > 0 ? dev_cu : 256;
-    }
-    WfParams W;
-    W.P = P;
-    W.ray = R->d_wf_ray;
-    W.path = R->d_wf_path;
-    W.remaining = R->d_wf_rem;
-    W.head = R->d_wf_ctr + 2;
-    W.refill = R->wf_refill;
-    int* q[2] = {R->d_wf_queue, R->d_wf_queue + n};
-    int* c[2] = {R->d_wf_ctr, R->d_wf_ctr + 1};
-    const dim3 block(256);
-    const dim3 g_trace(R->n_cu * 5), g_shade((unsigned)std::min<size_t>((n + 255) / 256, (size_t)R->n_cu * 8));
-    HIP_TRY(hipMemsetAsync(R->d_wf_ctr, 0, 4 * sizeof(int), st));
-    HIP_TRY(hipEventRecord(R->ev0, st));
-    W.initial = 1;
-    W.queue_in = nullptr;
-    W.count_in = c[1];
-    W.queue_out = q[0];
-    W.count_out = c[0];
-    if (cnt) hipLaunchKernelGGL((crt_wf_shade_kernel<true>), g_shade, block, 0, st, W);
-    else hipLaunchKernelGGL((crt_wf_shade_kernel<false>), g_shade, block, 0, st, W);
-    HIP_TRY(hipGetLastError());
-    W.initial = 0;
-    // every pixel's ray count is bounded: spp samples x (max_bounces + 1) segments, + slack
-    const long long max_iter = (long long)P.spp * (P.max_bounces + 2) + 4;
-    long long it = 0;
-    for (; it < max_iter; ++it) {
-        const int a = (int)(it & 1), b = a ^ 1;
-        W.queue_in = q[a];
-        W.count_in = c[a];
-        W.queue_out = q[b];
-        W.count_out = c[b];
-        if (cnt) {
-            hipLaunchKernelGGL((crt_wf_trace_kernel<true>), g_trace, block, 0, st, W);
-            hipLaunchKernelGGL((crt_wf_shade_kernel<true>), g_shade, block, 0, st, W);
-        } else {
-            hipLaunchKernelGGL((crt_wf_trace_kernel<false>), g_trace, block, 0, st, W);
-            hipLaunchKernelGGL((crt_wf_shade_kernel<false>), g_shade, block, 0, st, W);
-        }
-        HIP_TRY(hipGetLastError());
-        if ((it + 1) % R->wf_check == 0) {
-            HIP_TRY(hipMemcpyAsync(R->h_wf_count, c[b], sizeof(int), hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            if (*R->h_wf_count == 0) { ++it; break; }
-        }
-    }
-    R->wf_iterations = it;
-    HIP_TRY(hipEventRecord(R->ev1, st));
-    R->timed = true;
-    return CRT_OK;
-}
-
-int crt_renderer_set_wavefront(crt_renderer* R, int refill_lanes, int check_iterations) {
-    if (!R || refill_lanes < 1 || refill_lanes > 64 || check_iterations < 1 || check_iterations > 4096)
-        return set_error(CRT_ERR_INVALID_ARGUMENT, "refill 1..64, check 1..4096");
-    R->wf_refill = refill_lanes;
-    R->wf_check = check_iterations;
-    return CRT_OK;
-}
-
-long long crt_renderer_wavefront_iterations(const crt_renderer* R) { return R ? R->wf_iterations : -1; }
-
 // Cost-probe samples for a render of `spp` samples per pixel (0 = no probe).
 static int probe_spp_for(const crt_renderer* R, int spp) {
     if (spp < R->probe_min_spp || R->probe_spp == 0) return 0;
@@ -2986,16 +2520,16 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     if (S->device != R->device) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene and renderer on different devices");
     HIP_TRY(hipSetDevice(R->device));
     hipStream_t st = (hipStream_t)stream;
-    HIP_TRY(hipMemsetAsync(R->d_counters, 0, 16 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(R->d_counters, 0, ERR_WORD * sizeof(unsigned long long), st));   // the error word stays
     RenderParams P{};
     P.nodes = S->d_nodes; P.prims = S->d_prims; P.mats = S->d_mats; P.shade = S->d_shade;
     P.n_nodes = S->n_nodes; P.n_mats = S->n_mats; P.n_prims = S->n_prims; P.n_layouts = S->layouts;
-    P.err = reinterpret_cast<unsigned*>(R->d_counters + 7);
+    P.err = reinterpret_cast<unsigned*>(R->d_counters + ERR_WORD);
     P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
     P.accumulate = (flags & CRT_RENDER_ACCUMULATE) ? 1 : 0;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     P.ovf = nullptr;
-    P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0; P.tiles_per_wave = 1;
+    P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0;
     P.stack_cap = S->stack_cap;
     P.sphere_first = S->sphere_first;
     P.n_ray_spheres = S->n_ray_spheres;
@@ -3022,24 +2556,6 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     dim3 grid((R->width + 15) / 16, (R->height + 15) / 16), block(256);
     const bool cnt = (flags & CRT_RENDER_COUNT_WORK) != 0;
     P.regen_threshold = S->width == 4 ? R->regen_threshold_wide : R->regen_threshold;
-    if (S->width == 4 && R->variant == 5) {
-        P.stack_lds = std::min(R->stack_lds, WF_STACK);
-        if (S->stack_cap > P.stack_lds) {
-            const size_t need = (size_t)(S->stack_cap - P.stack_lds);
-            if (need * R->width * R->height * 4 >= ((size_t)1 << 32))
-                return set_error(CRT_ERR_INVALID_ARGUMENT, "traversal-stack overflow region would exceed 4 GiB");
-            if (need > R->ovf_entries) {
-                HIP_TRY(hipStreamSynchronize(st));
-                if (R->d_ovf) (void)hipFree(R->d_ovf);
-                R->d_ovf = nullptr;
-                R->ovf_entries = 0;
-                HIP_TRY(hipMalloc((void**)&R->d_ovf, need * R->width * R->height * 4));
-                R->ovf_entries = need;
-            }
-            P.ovf = R->d_ovf;
-        }
-        return render_wavefront(R, P, cnt, st);
-    }
     HIP_TRY(hipEventRecord(R->ev0, st));
 #define CRT_LAUNCH(V, W)                                                                     \
     do {                                                                                     \
@@ -3048,13 +2564,12 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, V, W>), grid, block, 0, st, P);  \
         else hipLaunchKernelGGL((crt_render_kernel<false, V, W>), grid, block, 0, st, P);     \
     } while (0)
-    // 4-wide scenes: variant 4 / 5 / 7 / 8 when selected explicitly; otherwise the measured best (profiles/r01w):
+    // 4-wide scenes: variant 4 / 7 / 8 when selected explicitly; otherwise the measured best (profiles/r01w):
     // 8 (probe-ordered tiles, one wave per workgroup) when the render runs the cost probe, 7 (lanes refill from a
     // pixel queue) for short renders such as the 1-spp interactive frames
     int wv = R->variant;
-    if (S->width == 4 && wv != 4 && wv != 5 && wv != 7 && wv != 8 && wv != 9)
-        wv = probe_spp_for(R, spp) > 0 ? 8 : 7;
-    if (S->width == 4 && (wv == 8 || wv == 9)) {
+    if (S->width == 4 && wv != 4 && wv != 7 && wv != 8) wv = probe_spp_for(R, spp) > 0 ? 8 : 7;
+    if (S->width == 4 && wv == 8) {
         const size_t n_pix = (size_t)R->width * R->height;
         const int tiles_x = (R->width + 7) / 8, n_tiles = tiles_x * ((R->height + 7) / 8);
         if (!R->d_tile_key) {
@@ -3069,15 +2584,11 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             HIP_TRY(hipMalloc((void**)&R->d_tile_key, (size_t)n_tiles * 4));
         }
         P.tiles_x = tiles_x;
-        P.order = nullptr;
-        const int per = (n_tiles + 7) / 8;
-        const int pspp = probe_spp_for(R, spp);
-        const bool probe = pspp > 0;
-        if (probe) {
-            // cost probe (variant 4, read-only) -> slowest pixel per tile -> tiles most expensive first (per XCD
-            // band when banded)
+        P.order = nullptr;     // no probe: tiles in row order
+        if (probe_spp_for(R, spp) > 0) {
+            // cost probe (variant 4, read-only) -> per-tile key -> tiles most expensive first
             RenderParams Q = P;
-            Q.spp = pspp;
+            Q.spp = probe_spp_for(R, spp);
             Q.accumulate = 0;
             Q.probe_cost = R->d_tile_cost;
             if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<true, 4, 6>), grid, block, 0, st, Q);
@@ -3089,51 +2600,17 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
                                    R->d_tile_key, tiles_x, n_tiles, R->d_tile_cost);
                 HIP_TRY(hipMemcpyAsync(R->d_tile_key, R->d_tile_cost, (size_t)n_tiles * 4, hipMemcpyDeviceToDevice, st));
             }
-            uint32_t* sorted = R->xcd_bands ? R->d_sorted : R->d_order;
-            if (R->xcd_bands && !sorted) {
-                HIP_TRY(hipStreamSynchronize(st));
-                HIP_TRY(hipMalloc((void**)&R->d_sorted, (size_t)n_tiles * 4));
-                sorted = R->d_sorted;
-            }
-            const int n_seg = R->xcd_bands ? 8 : 1, seg = R->xcd_bands ? per : n_tiles;
-            for (int k = 0; k < n_seg; ++k) {
-                const int b0 = k * seg, n = std::min(n_tiles, b0 + seg) - b0;
-                if (n <= 0) break;
-                const unsigned ob = (unsigned)((n + ORDER_ITEMS - 1) / ORDER_ITEMS);
-                HIP_TRY(hipMemsetAsync(R->d_order_hist, 0, ORDER_KEYS * 4, st));
-                hipLaunchKernelGGL(crt_order_hist_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key + b0, n, R->d_order_hist);
-                hipLaunchKernelGGL(crt_order_scan_kernel, dim3(1), dim3(ORDER_KEYS), 0, st, R->d_order_hist);
-                hipLaunchKernelGGL(crt_order_scatter_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key + b0, n,
-                                   R->d_order_hist, sorted + b0, (uint32_t)b0);
-            }
-            if (R->xcd_bands)
-                hipLaunchKernelGGL(crt_order_bands_kernel, dim3((8 * per + 255) / 256), dim3(256), 0, st, sorted,
-                                   n_tiles, per, R->d_order);
-            P.order = R->d_order;
-        } else if (R->xcd_bands) {
-            hipLaunchKernelGGL(crt_order_bands_kernel, dim3((8 * per + 255) / 256), dim3(256), 0, st, nullptr, n_tiles,
-                               per, R->d_order);
+            const unsigned ob = (unsigned)((n_tiles + ORDER_ITEMS - 1) / ORDER_ITEMS);
+            HIP_TRY(hipMemsetAsync(R->d_order_hist, 0, ORDER_KEYS * 4, st));
+            hipLaunchKernelGGL(crt_order_hist_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key, n_tiles, R->d_order_hist);
+            hipLaunchKernelGGL(crt_order_scan_kernel, dim3(1), dim3(ORDER_KEYS), 0, st, R->d_order_hist);
+            hipLaunchKernelGGL(crt_order_scatter_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key, n_tiles,
+                               R->d_order_hist, R->d_order, 0u);
             P.order = R->d_order;
         }
-        int n_wg = R->xcd_bands ? 8 * per : n_tiles;
-        if (wv == 9) {   // K tiles per wave; pad the order with empty tiles to a multiple of K
-            const int K = std::max(1, R->tiles_per_wave);
-            n_wg = (n_tiles + K - 1) / K;
-            P.tiles_per_wave = K;
-            if (!P.order) {
-                hipLaunchKernelGGL(crt_order_iota_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_order, n_tiles);
-                P.order = R->d_order;
-            }
-            if (n_wg * K > n_tiles)
-                HIP_TRY(hipMemsetAsync(R->d_order + n_tiles, 0xff, (size_t)(n_wg * K - n_tiles) * 4, st));
-        }
-        const dim3 tgrid(n_wg), tblock(64);
+        const dim3 tgrid(n_tiles), tblock(64);
         const char* cs = cnt ? "true" : "false";
-        if (wv == 9) {
-            std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 9, 6>", cs);
-            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 9, 6>), tgrid, tblock, 0, st, P);
-            else hipLaunchKernelGGL((crt_render_kernel<false, 9, 6>), tgrid, tblock, 0, st, P);
-        } else if (occ >= 7) {
+        if (occ >= 7) {
             std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 8, 7>", cs);
             if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 8, 7>), tgrid, tblock, 0, st, P);
             else hipLaunchKernelGGL((crt_render_kernel<false, 8, 7>), tgrid, tblock, 0, st, P);
@@ -3183,7 +2660,6 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         P.order = R->d_order;
         P.queue = R->d_queue;
         P.probe_cost = nullptr;
-        P.first_block_exclusive = R->first_block_exclusive;
         const int per_cu = occ >= 7 ? 7 : occ >= 6 ? 6 : 5;        // workgroups of 4 waves resident per CU
         const int n_wg = std::max(1, std::min(R->n_cus * per_cu, (int)((n_pix + 255) / 256)));
         const dim3 pgrid(n_wg);
@@ -3241,12 +2717,12 @@ int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene*
     if (A->n_ranks != B->n_ranks) return set_error(CRT_ERR_INVALID_ARGUMENT, "scenes hold different primitive sets");
     if (spp < 0 || max_bounces < 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "negative spp / bounces");
     HIP_TRY(hipSetDevice(R->device));
-    HIP_TRY(hipMemset(R->d_counters, 0, 16 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(R->d_counters, 0, ERR_WORD * sizeof(unsigned long long)));
     CompareParams Q{};
     RenderParams& P = Q.A;
     P.nodes = A->d_nodes; P.prims = A->d_prims; P.mats = A->d_mats; P.shade = A->d_shade;
     P.n_nodes = A->n_nodes; P.n_mats = A->n_mats; P.n_prims = A->n_prims; P.n_layouts = A->layouts;
-    P.err = reinterpret_cast<unsigned*>(R->d_counters + 7);
+    P.err = reinterpret_cast<unsigned*>(R->d_counters + ERR_WORD);
     P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
     P.accumulate = 0; P.regen_threshold = 64;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
@@ -3299,11 +2775,25 @@ int crt_renderer_render_frame(crt_renderer* R, const crt_scene* S, void* stream)
     return crt_renderer_synchronize(R, stream);
 }
 
+// The device error word (sticky across renders until read here): a render that dropped a traversal-stack entry
+// or met an out-of-range primitive index produced a wrong frame.  Reported where the reference reports a kernel
+// fault, at the synchronisation after the launch (CUDARenderer.cuh:59, CUDA_CHECK(cudaDeviceSynchronize())).
+static int take_device_error(crt_renderer* R, unsigned long long word) {
+    if (!word) return CRT_OK;
+    HIP_TRY(hipMemset(R->d_counters + ERR_WORD, 0, sizeof(unsigned long long)));
+    std::string m = "render kernel reported an internal error:";
+    if (word & 1u) m += " primitive index out of range;";
+    if (word & 2u) m += " traversal stack deeper than the scene's stack bound (entries dropped);";
+    return set_error(CRT_ERR_HIP, m + " the frame is invalid");
+}
+
 int crt_renderer_synchronize(crt_renderer* R, void* stream) {
     if (!R) return set_error(CRT_ERR_INVALID_ARGUMENT, "null renderer");
     HIP_TRY(hipSetDevice(R->device));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    return CRT_OK;
+    unsigned long long word = 0;
+    HIP_TRY(hipMemcpy(&word, R->d_counters + ERR_WORD, sizeof word, hipMemcpyDeviceToHost));
+    return take_device_error(R, word);
 }
 
 static int read_dev(crt_renderer* R, void* dst, const void* src, size_t bytes) {
@@ -3335,8 +2825,7 @@ int crt_renderer_get_counters(crt_renderer* R, crt_work_counters* out) {
     R->diag[0] = c[5]; R->diag[1] = c[6] & ((1ull << 40) - 1); R->diag[2] = c[6] >> 40;
     for (int i = 0; i < 7; ++i) R->prof[i] = c[8 + i];
     out->rays = c[0]; out->box_tests = c[1]; out->tri_tests = c[2]; out->sphere_tests = c[3]; out->paths = c[4];
-    if (c[7]) return set_error(CRT_ERR_HIP, "render kernel reported an internal indexing error");
-    return CRT_OK;
+    return take_device_error(R, c[ERR_WORD]);
 }
 int crt_renderer_get_section_profile(crt_renderer* R, unsigned long long* out7) {
     if (!R || !out7) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");

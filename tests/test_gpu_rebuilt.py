@@ -139,37 +139,7 @@ def test_golden_fixture_rebuilt(rebuilt):
     _compare(r.linear(), g["sum"], 16, 0.99)
 
 
-@pytest.mark.parametrize("refill", [1, 16, 64])
-def test_wavefront_equals_megakernel(rebuilt, refill):
-    """Variant 5 (trace / shade kernels over a pixel queue) == variant 4, bit for bit, incl. accumulate."""
-    w, h, spp = 160, 90, 8
-    cam = crt_amd.camera(spp)
-    dev = rebuilt["cornell_bunny", "w4"]
-    a = _frame(dev, w, h, spp, 20, cam, variant=3)
-    b = crt_amd.Renderer(w, h)
-    b.set_kernel_variant(5)
-    b.set_wavefront(refill, 4)
-    b.set_camera(cam)
-    b.init_rand(41)
-    b.render(dev, 3, 20)
-    b.render(dev, 5, 20, accumulate=True)
-    b.synchronize()
-    assert b.wavefront_iterations() > 0
-    assert np.array_equal(a.linear().view(np.uint32), b.linear().view(np.uint32))
-    assert np.array_equal(a.rng_state(), b.rng_state())
-    c = crt_amd.Renderer(w, h)
-    c.set_kernel_variant(5)
-    c.set_stack_lds(1)
-    c.set_camera(cam)
-    c.init_rand(41)
-    c.render(dev, spp, 20, count_work=True)
-    c.synchronize()
-    assert np.array_equal(a.linear().view(np.uint32), c.linear().view(np.uint32))
-    assert c.counters()["rays"] == a.counters()["rays"]
-
-
-
-@pytest.mark.parametrize("variant", [7, 8, 9])
+@pytest.mark.parametrize("variant", [7, 8])
 @pytest.mark.parametrize("w,h,spp", [(160, 90, 8), (100, 37, 70), (64, 36, 0), (1, 1, 64), (9, 1, 65), (1, 17, 3)])
 def test_persistent_queue_variant_is_bit_identical(rebuilt, w, h, spp, variant):
     """Variants 7 (lanes take pixels from a global queue in probe-cost order) and 8 (one wave per workgroup, 8x8
@@ -193,7 +163,7 @@ def test_persistent_queue_variant_is_bit_identical(rebuilt, w, h, spp, variant):
     assert np.array_equal(a.rng_state(), b.rng_state())
 
 
-@pytest.mark.parametrize("variant", [7, 8, 9])
+@pytest.mark.parametrize("variant", [7, 8])
 def test_persistent_queue_counting_kernel(rebuilt, variant):
     dev = rebuilt["cornell_bunny", "w4"]
     cam = crt_amd.camera(4)
@@ -213,22 +183,9 @@ def test_persistent_queue_counting_kernel(rebuilt, variant):
 
 
 @pytest.mark.parametrize("probe_spp", [0, 4])
-def test_xcd_band_order_is_bit_identical(rebuilt, probe_spp):
-    """Variant 8 with the XCD-band work order (each XCD one horizontal strip; padding slots for a tile count
-    that is not a multiple of 8)."""
-    _schedule_case(rebuilt, 8, probe_spp, xcd_bands=True)
-
-
-@pytest.mark.parametrize("probe_spp", [0, 4])
-def test_first_block_exclusive_is_bit_identical(rebuilt, probe_spp):
-    """Variant 7 whose waves refill only after their first 64 pixels are done."""
-    _schedule_case(rebuilt, 7, probe_spp, first_block=True)
-
-
-@pytest.mark.parametrize("k", [1, 3])
-def test_tiles_per_wave_is_bit_identical(rebuilt, k):
-    """Variant 9 with K tiles per wave (78 tiles: K = 3 pads the last wave)."""
-    _schedule_case(rebuilt, 9, 4, tiles_per_wave=k)
+def test_probe_order_is_bit_identical(rebuilt, probe_spp):
+    """Variant 8 with and without the cost probe (row order / most expensive tiles first)."""
+    _schedule_case(rebuilt, 8, probe_spp)
 
 
 @pytest.mark.parametrize("key", [1, 2])
@@ -239,7 +196,7 @@ def test_tile_key_modes_are_bit_identical(rebuilt, key):
 def _schedule_case(rebuilt, variant, probe_spp, **flags):
     """A schedule option, with and without the cost probe: the same frame and RNG state as variant 4."""
     dev = rebuilt["cornell_bunny", "w4"]
-    w, h, spp = 104, 45, 64          # 13 x 6 = 78 tiles: bands of 10, the last two short
+    w, h, spp = 104, 45, 64          # 13 x 6 = 78 tiles, the last row partial
     cam = crt_amd.camera(spp)
     a = _frame(dev, w, h, spp, 20, cam, variant=4)
     b = crt_amd.Renderer(w, h)

@@ -70,9 +70,7 @@ for cfg in a.configs.split(","):
         r.set_occupancy_target(occ)
         r.set_regen_threshold(int(f.get("T", 24)))
         r.set_kernel_variant(int(f.get("V", 3)))
-        r.set_schedule(int(f.get("P", -1)), 64, bool(int(f.get("X", 0))), bool(int(f.get("F", 0))), int(f.get("K", 2)),
-                       int(f.get("Y", 2)))
-        r.set_wavefront(int(f.get("R", 16)), int(f.get("K", 16)))
+        r.set_schedule(int(f.get("P", -1)), 64, int(f.get("Y", 2)))
         t = time.time()
         sc = hs.upload(0, bvh="rebuilt", leaf_size=leaf, layouts=layouts, traversal_cost=trav, width=width)
         build_s = time.time() - t
@@ -88,7 +86,6 @@ for cfg in a.configs.split(","):
                "image": {"pixels_bit_equal": float(np.mean(np.all(img == img_ref, axis=-1))),
                          "rms_per_channel": [float(x) for x in np.sqrt(np.mean(d.reshape(-1, 3) ** 2, axis=0))]}}
         out["schedule"] = r.schedule_stats()
-        out["wf_iterations"] = r.wavefront_iterations()
         prof = r.section_profile()
         tot = max(1, prof["cyc_regen"] + prof["cyc_step"] + prof["cyc_round"])
         out["section_profile"] = dict(prof, frac_regen=round(prof["cyc_regen"] / tot, 3),

@@ -1,0 +1,43 @@
+#!/bin/bash
+# One parameterised GPU job for gpurun (run from the repo root on the GPU box). Every GPU step has its own time
+# limit and the steps are chained with set -e, so a failing or hung step ends the job.
+#
+#   tools/gpu_job.sh check OUT            GPU tests, smoke, default bench, rocprofv3 kernel stats of the bench
+#   tools/gpu_job.sh bench OUT [ARGS..]   bench.py ARGS, then the same under rocprofv3 --kernel-trace --stats
+#   tools/gpu_job.sh ab OUT LIB_B [N] [ARGS..]
+#                                         A/B of the in-tree libcrt_hip.so (A) against LIB_B (a build from
+#                                         tools/build_profile_lib.sh), N alternating A B rounds of bench.py ARGS
+#   tools/gpu_job.sh pmc OUT [ARGS..]     rocprofv3 --pmc passes (tools/pmc.sh) over one bench frame
+set -e
+MODE=$1; OUT=gpurun_out/$2; shift 2
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p $R/$OUT
+case $MODE in
+check)
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $R/$OUT/pytest_gpu.log 2>&1
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $R/$OUT/smoke.log 2>&1
+  timeout -k 10 400 python3 bench.py > $R/$OUT/bench.log 2>&1
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof -o bench -- \
+      python3 $R/bench.py --no-cpu-baseline --no-parity > $R/$OUT/bench_prof.log 2>&1
+  ;;
+bench)
+  timeout -k 10 600 python3 bench.py "$@" > $R/$OUT/bench.log 2>&1
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof -o bench -- \
+      python3 $R/bench.py --no-cpu-baseline --no-parity "$@" > $R/$OUT/bench_prof.log 2>&1
+  ;;
+ab)
+  LIBB=$1; N=${2:-2}; shift 2
+  for i in $(seq 1 $N); do
+    timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-count --no-parity "$@" > $R/$OUT/bench_A$i.log 2>&1
+    CRT_HIP_LIB=$R/$LIBB timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-count --no-parity "$@" \
+        > $R/$OUT/bench_B$i.log 2>&1
+  done
+  ;;
+pmc)
+  bash tools/pmc.sh $OUT "$@"
+  ;;
+*) echo "unknown mode $MODE"; exit 2 ;;
+esac
+echo "gpu_job $MODE done"
