@@ -176,7 +176,10 @@ typedef struct crt_scene_options {
                                  2 = threaded binary layouts (variants 0-3) */
     int32_t gpu_build;        /* REBUILT: 1 = build the binned-SAH tree on the GPU (crt_scene_create_ex: the scene's
                                  device; crt_scene_export: device 0), 0 = on the host (default) */
-    int32_t reserved[2];
+    int32_t stack_cap;        /* REBUILT width 4: 0 = the traversal-stack bound computed from the tree (default); > 0
+                                 overrides it.  Testing only: a value below the bound makes a render that needs more
+                                 entries report CRT_ERR_HIP at synchronisation (the entries are dropped). */
+    int32_t reserved;
 } crt_scene_options;
 
 /* ---- scene (SceneManager device half) ---- */

@@ -63,6 +63,11 @@ class MeshDesc(C.Structure):
                 ("nodes", C.c_void_p), ("node_count", C.c_int32), ("aabb", C.c_float * 6)]
 
 
+class MaterialDesc(C.Structure):      # crt_hip.h crt_material_desc
+    _fields_ = [("type", C.c_int32), ("albedo", C.c_float * 3), ("emission", C.c_float * 3), ("roughness", C.c_float),
+                ("ior", C.c_float)]
+
+
 class SceneStats(C.Structure):
     _fields_ = [("device_nodes", C.c_int64), ("device_prims", C.c_int64), ("device_bytes", C.c_int64),
                 ("max_depth", C.c_int32), ("n_materials", C.c_int32), ("bvh", C.c_int32), ("layouts", C.c_int32),
@@ -72,7 +77,7 @@ class SceneStats(C.Structure):
 class SceneOptions(C.Structure):
     _fields_ = [("bvh", C.c_int32), ("leaf_size", C.c_int32), ("layouts", C.c_int32),
                 ("traversal_cost", C.c_float), ("width", C.c_int32), ("gpu_build", C.c_int32),
-                ("reserved", C.c_int32 * 2)]
+                ("stack_cap", C.c_int32), ("reserved", C.c_int32)]
 
 
 BVH_REFERENCE = 0

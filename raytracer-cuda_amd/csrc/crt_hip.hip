@@ -2305,7 +2305,7 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
     S->max_depth = rebuilt ? RB.max_depth : F.max_depth;
     S->excluded = rebuilt ? RB.excluded : 0;
     S->width = rebuilt ? RB.width : 2;
-    S->stack_cap = rebuilt ? RB.stack_bound : 0;
+    S->stack_cap = rebuilt ? (o.stack_cap > 0 ? o.stack_cap : RB.stack_bound) : 0;
     S->sphere_first = rebuilt ? RB.sphere_first : 0;
     {
         int in_tree = 0;   // spheres the 4-wide tree itself holds (not tested per ray)
