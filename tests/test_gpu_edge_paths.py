@@ -144,7 +144,7 @@ def test_edge_scenes_exercise_the_paths(edge_scenes):
     hs, _, _, _, _ = edge_scenes["fuzzy_metal"]
     _, _, fm, info, mats = hs.loader_arrays()
     metal = mats[mats[:, 0] == 1]                        # MaterialType::Metal rows: type, albedo3, emission3, r, ior
-    assert sorted(np.round(metal[:, 7], 6).tolist()) == [0.25, 0.3]   # sqrt(2/(30+2)) and Pr 0.3
+    assert np.allclose(np.sort(metal[:, 7]), [0.25, 0.3])   # sqrt(2/(30+2)) and Pr 0.3
     assert info[1, 5] == 8                               # 2 files: offset = Cornell's 8 materials -> the metals
     hs3, _, _, _, _ = edge_scenes["three_objs"]
     _, _, fm3, info3, mats3 = hs3.loader_arrays()

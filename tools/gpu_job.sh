@@ -8,6 +8,7 @@
 #                                         A/B of the in-tree libcrt_hip.so (A) against LIB_B (a build from
 #                                         tools/build_profile_lib.sh), N alternating A B rounds of bench.py ARGS
 #   tools/gpu_job.sh pmc OUT [ARGS..]     rocprofv3 --pmc passes (tools/pmc.sh) over one bench frame
+#   tools/gpu_job.sh l1 OUT               vector-L1 calibration micro-benchmark (tools/probes/l1_probe.hip) + PMC
 set -e
 MODE=$1; OUT=gpurun_out/$2; shift 2
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -37,6 +38,13 @@ ab)
   ;;
 pmc)
   bash tools/pmc.sh $OUT "$@"
+  ;;
+l1)
+  # vector-L1 calibration (tools/probes/l1_probe.hip, built on the CPU side): timings, then one PMC pass
+  timeout -k 10 120 tools/probes/l1_probe > $R/$OUT/l1_probe.log 2>&1
+  cd /tmp && export TMPDIR=/tmp
+  timeout -s KILL 120 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES TCP_PENDING_STALL_CYCLES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE \
+      --output-format csv -d $R/$OUT/pmc -o l1 -- $R/tools/probes/l1_probe > $R/$OUT/l1_pmc.log 2>&1
   ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
 esac
