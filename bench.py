@@ -31,7 +31,32 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parent
 sys.path[:0] = [str(REPO / "raytracer-cuda_amd"), str(REPO)]
 
-METRIC = "Mrays/sec + frame wall-clock, Cornell+bunny 2560×1440 2000spp 20bounce"
+# BASELINE.json `metric` for the headline config; other configs get the same metric with their own workload label
+SCENE_LABEL = {"cornell": "Cornell", "cornell_bunny": "Cornell+bunny", "cornell_1m": "1M-triangle bunny-x10",
+               "cornell_metal": "Cornell+metal blocks", "cornell_bunny_metal": "Cornell+bunny+metal blocks"}
+SCENE_DATA = {
+    "cornell": "synthetic: authored Cornell box OBJ (the reference git-ignores its assets)",
+    "cornell_bunny": "synthetic: authored Cornell box OBJ + seeded 69,300-triangle glass bunny-proxy OBJ "
+                     "(the reference git-ignores its assets)",
+    "cornell_1m": "synthetic: authored Cornell box OBJ + one OBJ of 10 translated seeded 100k-triangle bunny proxies "
+                  "(1.0M triangles, one mesh)",
+    "cornell_metal": "synthetic: authored Cornell box OBJ + authored fuzzy-metal blocks OBJ",
+    "cornell_bunny_metal": "synthetic: authored Cornell box, glass bunny-proxy and fuzzy-metal blocks OBJs",
+}
+# BASELINE.json configs this bench reproduces: (scene, W, H, spp, bounces) -> index
+BASELINE_CONFIGS = {("cornell", 256, 256, 16, 4): 0, ("cornell_bunny", 1280, 720, 256, 20): 1,
+                    ("cornell_bunny", 2560, 1440, 2000, 20): 2, ("cornell_1m", 2560, 1440, 512, 20): 4}
+
+
+def metric_name(args) -> str:
+    return (f"Mrays/sec + frame wall-clock, {SCENE_LABEL[args.scene]} {args.width}×{args.height} "
+            f"{args.spp}spp {args.bounces}bounce")
+
+
+def workload_name(args) -> str:
+    w = f"{args.scene} {args.width}x{args.height} {args.spp}spp {args.bounces} bounces"
+    k = BASELINE_CONFIGS.get((args.scene, args.width, args.height, args.spp, args.bounces))
+    return w + (f" (configs[{k}])" if k is not None else "")
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_TOPS = 157.3 / 2       # f32 vector: 157.3 TFLOP/s counts an FMA as 2; the path has no FMA
 
@@ -50,7 +75,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="cornell_bunny", choices=["cornell", "cornell_bunny", "cornell_1m"])
+    ap.add_argument("--scene", default="cornell_bunny", choices=sorted(SCENE_LABEL))
     ap.add_argument("--width", type=int, default=2560)
     ap.add_argument("--height", type=int, default=1440)
     ap.add_argument("--spp", type=int, default=2000)
@@ -59,6 +84,9 @@ def parse():
     ap.add_argument("--no-count", action="store_true", help="skip the work-counting launch (roofline -> null)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0 = min(16, usable cores), the GPU box's CPU share; 1 = the "
+                         "single-thread reference path of BASELINE.json configs[0])")
     ap.add_argument("--save-ppm", default="", help="rank 0 writes the resolved frame here")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--kernel-variant", type=int, default=None, help="render-kernel variant (default: library's)")
@@ -73,9 +101,20 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, cam_floats, log_fn):
-    """Oracle (C restatement of the reference path, kind 'port') on this host's cores, bounded sample:
-    the full frame at a reduced spp chosen so the run takes about args.cpu_seconds."""
+    """The oracle (oracle/crt_oracle.c, the C restatement of the reference's render path; kind 'port': the reference
+    itself needs CUDA/cuRAND/SFML and cannot be built here) on this host's cores.  Bounded sample: the
+    exact workload when it fits in about args.cpu_seconds, else the full frame at a reduced spp sized to that."""
     sys.path.insert(0, str(REPO / "oracle"))
     import objload
     import pyoracle
@@ -84,29 +123,39 @@ def cpu_baseline(args, cam_floats, log_fn):
         ncpu = len(os.sched_getaffinity(0))
     except AttributeError:
         ncpu = os.cpu_count() or 1
-    threads = max(1, min(16, ncpu))
+    threads = args.cpu_threads if args.cpu_threads > 0 else max(1, min(16, ncpu))
     sc = pyoracle.OracleScene(objload.load_scene(assets.scene_files(args.scene)))
     w, h = args.width, args.height
     t = time.perf_counter()
     _, _, c1 = sc.render(cam_floats, w, h, 1, args.bounces, seed=args.seed, nthreads=threads)
     t1 = time.perf_counter() - t
-    spp = int(max(1, min(64, round(args.cpu_seconds / max(t1, 1e-3)))))
+    if t1 * args.spp <= 1.5 * args.cpu_seconds:            # the whole workload fits: run it exactly
+        spp = args.spp
+    else:
+        spp = int(max(1, min(64, round(args.cpu_seconds / max(t1, 1e-3)))))
     c, dt = c1, t1
     for _ in range(2):   # the 1-spp calibration includes one-time start-up cost: re-aim from the warm run
-        if spp <= 1 or spp > 64:
+        if spp == 1 and args.spp != 1:
             break
         t = time.perf_counter()
         _, _, c = sc.render(cam_floats, w, h, spp, args.bounces, seed=args.seed, nthreads=threads)
         dt = time.perf_counter() - t
+        if spp == args.spp:
+            break
         nxt = int(max(1, min(64, round(spp * args.cpu_seconds / max(dt, 1e-3)))))
         if dt >= 0.6 * args.cpu_seconds or nxt <= spp:
             break
         spp = nxt
+    full = spp == args.spp
     log_fn(f"[cpu] oracle {w}x{h} {spp}spp: {c['rays']} rays in {dt:.2f}s on {threads} threads")
     return {"value": round(c["rays"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"full {w}x{h} frame, {spp} spp/pixel, {args.bounces} bounces, seed {args.seed} "
-                      f"(same scene + camera as the GPU run; {c['rays']} rays in {dt:.2f} s)",
-            "frame_wall_s_extrapolated": round(dt * args.spp / spp, 1)}
+            "what": "oracle/crt_oracle.c: C restatement of the reference's render path (bit-identical to the GPU "
+                    "reference-BVH frames); the reference itself needs CUDA/cuRAND/SFML and cannot be built here",
+            "cpu_model": cpu_model(), "usable_cores": ncpu,
+            "sample": (f"the whole workload: {w}x{h}, {spp} spp/pixel, {args.bounces} bounces, seed {args.seed}" if full
+                       else f"full {w}x{h} frame at {spp} of {args.spp} spp/pixel, {args.bounces} bounces, seed "
+                            f"{args.seed}") + f" (same scene + camera as the GPU run; {c['rays']} rays in {dt:.2f} s)",
+            "frame_wall_s" if full else "frame_wall_s_extrapolated": round(dt * args.spp / spp, 3)}
 
 
 def pmc_traffic(workload_key: str):
@@ -299,13 +348,11 @@ def main():
     value = rays_frame * args.steps / elapsed / 1e6
     if rank == 0:
         out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world,
+            "metric": metric_name(args), "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: authored Cornell box OBJ + seeded 69,300-triangle glass bunny-proxy OBJ "
-                    "(the reference git-ignores its assets)",
-            "config": {"workload": f"{args.scene} {W}x{H} {args.spp}spp {args.bounces} bounces (configs[2])"
-                       if args.scene == "cornell_bunny" else f"{args.scene} {W}x{H} {args.spp}spp {args.bounces} bounces",
+            "data": SCENE_DATA[args.scene],
+            "config": {"workload": workload_name(args),
                        "width": W, "height": H, "spp": args.spp, "max_bounces": args.bounces, "seed": args.seed,
                        "triangles": counts["n_indices"] // 3, "bvh": bvh_desc, "kernel_variant": variant,
                        "parallelism": f"spp-shard x{world}" + ((" + RCCL reduce of fp32 framebuffer" if args.dist_backend == "nccl"

@@ -15,7 +15,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/$OUT
 case $MODE in
 check)
-  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $R/$OUT/pytest_gpu.log 2>&1
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $R/$OUT/pytest_gpu.log 2>&1
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $R/$OUT/smoke.log 2>&1
   timeout -k 10 400 python3 bench.py > $R/$OUT/bench.log 2>&1
   cd /tmp && export TMPDIR=/tmp
