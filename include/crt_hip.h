@@ -57,7 +57,7 @@ typedef struct crt_material_desc {
     float ior;
 } crt_material_desc;
 
-/* One reference BVHNode (BVHNode.cuh:347-354 fields): box + children / leaf range. */
+/* One reference BVHNode (BVHNode.cuh:158-165 fields): box + children / leaf range. */
 typedef struct crt_bvh_node_desc {
     float bmin[3];
     float bmax[3];
@@ -86,7 +86,7 @@ typedef struct crt_sphere_desc {
 } crt_sphere_desc;
 
 enum crt_object_kind { CRT_OBJECT_MESH = 0, CRT_OBJECT_SPHERE = 1 };
-typedef struct crt_object_desc {   /* HittableList::m_Objects entry (HittableList.cuh:331) */
+typedef struct crt_object_desc {   /* HittableList::m_Objects entry (HittableList.cuh:73) */
     int32_t kind;
     int32_t index;                 /* into meshes[] or spheres[] */
 } crt_object_desc;

@@ -28,7 +28,7 @@
  *       - pow(float,int) in Dielectric::schlicksReflectance (Material.cuh:136):
  *         CUDA's pow(float,int) overload; restated as exponentiation by squaring.
  *       - Argument evaluation order of Vec3(randomFloat(),randomFloat(),...)
- *         (Utility.cuh:190-192, :208) taken left-to-right.
+ *         (Utility.cuh:40-42, :58) taken left-to-right.
  *       - nvcc's default -fmad=true contraction is NOT modelled (it is not
  *         reproducible across compilers); the oracle is the no-contraction path.
  */
@@ -298,7 +298,7 @@ static int mat_scatter(const Mat* m, const Ray* in, const Hit* h, V3* att, Ray* 
 static V3 mat_emit(const Mat* m) { return m->type == MT_LIGHT ? m->emission : v3(0, 0, 0); } /* :53-55, :144 */
 
 /* ------------------------------------------------------------ BVH nodes */
-/* Core/BVHNode.cuh:198-355 (the subset used by Mesh and the scene) */
+/* Core/BVHNode.cuh:9-166 (the subset used by Mesh and the scene) */
 typedef struct { Box box; int left, right, obj_index, obj_count, is_leaf; } Node;
 
 /* ------------------------------------------------------------------ Mesh */
@@ -546,7 +546,7 @@ static void build_scene_bvh(Scene* sc) {                                        
     }
     sc->n_snodes = next + 1;
 }
-static int scene_hit(const Scene* sc, const Ray* r, Iv rt, Hit* rec, Counters* cn) {        /* BVHNode.cuh:304-345 */
+static int scene_hit(const Scene* sc, const Ray* r, Iv rt, Hit* rec, Counters* cn) {        /* BVHNode.cuh:115-156 */
     int any = 0;
     float closest = rt.max;
     uint32_t stack[MAX_STACK_SIZE / 2];

@@ -16,12 +16,12 @@ namespace crt {
 // nodes: 2 x float4 (32 B) per node, DFS preorder over the scene BVH with every
 // mesh BVH spliced in after its scene leaf ("threaded" BVH: left child = next
 // node, `skip` = first node after the subtree).  The left-first stack DFS of
-// BVHNode::hit (BVHNode.cuh:304-345) and Mesh::hit (Mesh.cuh:55-110) visits
+// BVHNode::hit (BVHNode.cuh:115-156) and Mesh::hit (Mesh.cuh:55-110) visits
 // exactly this order, so the traversal needs no stack at all.
 //   A = (min.x, min.y, min.z, max.x)   B = (max.y, max.z, a, b)
 //   internal mesh node : a = skip, b = NODE_MESH_INNER  (box tested against [0.001, closest])
 //   scene node / scene mesh leaf : a = skip, b = NODE_SCENE_INNER (box tested against [0.001, inf),
-//                                   the unshrunk ray_t of BVHNode::hit, BVHNode.cuh:318)
+//                                   the unshrunk ray_t of BVHNode::hit, BVHNode.cuh:129)
 //   mesh leaf          : a = triangle count, b = first triangle prim (>= 0)
 //   sphere leaf        : a = 0, b = SPHERE_BIT | sphere prim          (scene level: [0.001, inf))
 //   every leaf continues at node + 1.
@@ -107,10 +107,10 @@ __device__ __forceinline__ float uniform(Rng& s) {
     const float inv = 2.3283064e-10f;   // CURAND_2POW32_INV
     return (float)next_u32(s) * inv + (inv / 2.0f);
 }
-// Utility.cuh:168-171: min + (max - min) * U, here min=-1, max=1.
+// Utility.cuh:18-21: min + (max - min) * U, here min=-1, max=1.
 __device__ __forceinline__ float rand_pm1(Rng& s) { return -1.0f + 2.0f * uniform(s); }
 
-__device__ __forceinline__ V3 rand_unit_vector(Rng& s) {   // Utility.cuh:195-203, :223-226
+__device__ __forceinline__ V3 rand_unit_vector(Rng& s) {   // Utility.cuh:45-53, :73-76
     V3 p;
     for (;;) {
         float a = rand_pm1(s);

@@ -47,7 +47,6 @@ struct RenderParams {
     const float4* __restrict__ mats;
     const float4* __restrict__ shade;     // per reference DFS rank: shading record (crt_device.h)
     int n_nodes, n_mats, n_prims;         // n_nodes: nodes of ONE threaded layout
-    uint32_t prim_plane;                  // 4-wide scenes: bytes per primitive plane (prim_rec); 0 otherwise
     int n_layouts;                        // 1, or 6 direction-ordered layouts (CRT_BVH_REBUILT)
     uint32_t* __restrict__ ovf;           // variant 4: traversal-stack entries beyond the LDS part
     int stack_cap;                        // variant 4: stack entries a ray can need (host bound)
@@ -104,7 +103,7 @@ __device__ __forceinline__ int layout_base(V3 d, int n_layouts, int n_nodes) {
 
 // Closest hit over the threaded scene+mesh BVH.  Returns the reference DFS rank of the hit primitive
 // or -1; `closest` = IntersectionTime of the accepted hit.
-// Semantics: BVHNode::hit (BVHNode.cuh:304-345), Mesh::hit (Mesh.cuh:55-110),
+// Semantics: BVHNode::hit (BVHNode.cuh:115-156), Mesh::hit (Mesh.cuh:55-110),
 // AABB::hit (AABB.cuh:123-146), rayTriangleIntersect (Mesh.cuh:266-308),
 // Sphere::hit (Sphere.cuh:27-47); closed-interval acceptance so ties go to the
 // later primitive, exactly as in the reference order.
@@ -298,23 +297,12 @@ __device__ __forceinline__ const float4* rec_at(const float4* base, uint32_t byt
     return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + byte_off);
 }
 
-// 4-wide scenes keep the primitive records as three planes of float4: word group k of primitive p at byte
-// k * plane + 16 p (plane = 16 * primitives, below 4 GiB).  The pairs of a leaf round are mostly consecutive primitives
-// of a few leaves, so each of the three loads reads contiguous 16-B words instead of 16 B out of every 48 — a third of
-// the cache-line lookups.
-__device__ __forceinline__ void prim_rec(const float4* __restrict__ prims, uint32_t plane, int p, float4& f0, float4& f1,
-                                         float4& f2) {
-    const char* b = reinterpret_cast<const char*>(prims);
-    const uint32_t off = (uint32_t)p * 16u;
-    f0 = *reinterpret_cast<const float4*>(b + off);
-    f1 = *reinterpret_cast<const float4*>(b + plane + off);
-    f2 = *reinterpret_cast<const float4*>(b + 2 * (size_t)plane + off);
-}
-
-__device__ __forceinline__ float prim_test(const float4* __restrict__ prims, uint32_t plane, int p, V3 o, V3 d,
-                                           float tmax, int& rank, bool tree_spheres = true) {
-    float4 f0, f1, f2;
-    prim_rec(prims, plane, p, f0, f1, f2);
+// (Storing the records as three planes of float4, for contiguous 16-B words per load, measured 2.7 % slower: the three
+// planes are three cache lines per triangle where the 48-B record mostly sits in one, profiles/r02c.)
+__device__ __forceinline__ float prim_test(const float4* __restrict__ prims, int p, V3 o, V3 d, float tmax, int& rank,
+                                           bool tree_spheres = true) {
+    const float4* r = rec_at(prims, (uint32_t)p * 48u);
+    const float4 f0 = r[0], f1 = r[1], f2 = r[2];
     rank = __float_as_int(f2.z);
     if (tree_spheres && __float_as_int(f2.w) == 1) return sphere_candidate(f0, f1, o, d, tmax);
     return tri_test_rec(f0, f1, f2, o, d, tmax);
@@ -672,17 +660,17 @@ __device__ __forceinline__ void ray_spheres2(const float* sa, const float* sb, V
 
 // inv: AABB::hit's 1/d, bit-exact (recip_exact_any), shared with the traversal.
 template <bool LATE = false>
-__device__ __forceinline__ void ray_spheres(const float4* __restrict__ prims, uint32_t plane,
-                                            const float4* __restrict__ chain, int n_chain, int first, int n, V3 o, V3 d,
-                                            V3 inv, float& closest, int& hit, const float* sph2 = nullptr) {
+__device__ __forceinline__ void ray_spheres(const float4* __restrict__ prims, const float4* __restrict__ chain,
+                                            int n_chain, int first, int n, V3 o, V3 d, V3 inv, float& closest,
+                                            int& hit, const float* sph2 = nullptr) {
     if (n == 0) return;
     if (n == 2 && sph2) {
         ray_spheres2<LATE>(sph2, sph2 + 12, o, d, inv, closest, hit);
         return;
     }
     for (int s = 0; s < n; ++s) {
-        float4 f0, f1, f2;
-        prim_rec(prims, plane, first + s, f0, f1, f2);
+        const int p = first + s;
+        const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1];
         const int k = __float_as_int(f1.w);
         if (!ref_scene_box(chain[2 * k], chain[2 * k + 1], o, inv)) continue;
         const float t = sphere_candidate(f0, f1, o, d, __builtin_inff());
@@ -701,13 +689,13 @@ __device__ __forceinline__ void cas(uint32_t& a, uint32_t& b) {
 }
 
 // Per-lane closest hit over a 4-wide BVH (diagnostic path: crt_scene_compare).  Returns the rank or -1.
-__device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict__ prims, uint32_t plane,
+__device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                       const float4* __restrict__ chain, int n_chain, int sphere_first, int n_spheres, V3 o, V3 d,
                       float& closest) {
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     closest = __builtin_inff();
     int hit = -1, node = 0, sp = 0;
-    ray_spheres(prims, plane, chain, n_chain, sphere_first, n_spheres, o, d, inv, closest, hit);
+    ray_spheres(prims, chain, n_chain, sphere_first, n_spheres, o, d, inv, closest, hit);
     int stack[64];
     while (node >= 0) {
         const float4* q = nodes + 8 * (size_t)node;
@@ -722,7 +710,7 @@ __device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict
             if (s >= n_int && c > 0 && w.hit[s]) {
                 for (int k = 0; k < c; ++k) {
                     int rank;
-                    const float t = prim_test(prims, plane, __float_as_int(mf.z) + off + k, o, d, entry, rank);
+                    const float t = prim_test(prims, __float_as_int(mf.z) + off + k, o, d, entry, rank);
                     if (t >= 0.f && better(t, rank, closest, hit)) { closest = t; hit = rank; }
                 }
             }
@@ -873,7 +861,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
             if (COUNT) cnt.tris++;
             if ((unsigned)p < (unsigned)P.n_prims) {
                 int rank;
-                const float t = prim_test(P.prims, P.prim_plane, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
+                const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
                                           P.tree_spheres != 0);
                 if (t >= 0.f)
                     atomicMin(&L.key[owner], ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank));
@@ -1132,7 +1120,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 if (COUNT) cnt.passes++;
                 if (parked) {
                     if (has_result)
-                        ray_spheres<true>(P.prims, P.prim_plane, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
+                        ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
                                           sphere_inv(S.d, inv), closest, hit, sph_lds);
                     if (has_result) shade(S, P, hit, closest);
                     live = next_ray(S, C, px, py, P.max_bounces);
@@ -1227,7 +1215,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     // (loading the shading record before this sphere test, to overlap its latency, measured +0.7 %:
                     // profiles/r01ar)
                     if (has_result)
-                        ray_spheres<true>(P.prims, P.prim_plane, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
+                        ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
                                           sphere_inv(S.d, inv), closest, hit, sph_lds);
                     if (has_result) shade(S, P, hit, closest);
                     const uint64_t s1 = COUNT ? shader_clock() : 0;
@@ -1369,7 +1357,6 @@ struct CompareParams {
     RenderParams A;
     const float4* __restrict__ nodes_b;
     const float4* __restrict__ prims_b;
-    uint32_t prim_plane_b;                // width-4 scene B: primitive plane bytes (prim_rec)
     int n_nodes_b, n_layouts_b;
     int width_a, width_b;
     int sphere_first_b, n_spheres_b;
@@ -1409,12 +1396,12 @@ __global__ __launch_bounds__(256) void crt_compare_kernel(CompareParams Q) {
     while (next_ray(S, C, x, y, P.max_bounces)) {
         ++S.rays;
         float ta, tb;
-        const int ha = Q.width_a == 4 ? trace4(P.nodes, P.prims, P.prim_plane, P.sphere_chain, P.n_chain, P.sphere_first,
-                                               P.n_ray_spheres, S.o, S.d, ta)
+        const int ha = Q.width_a == 4 ? trace4(P.nodes, P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres,
+                                               S.o, S.d, ta)
                                       : trace<false>(P.nodes, P.prims, P.n_nodes, layout_base(S.d, P.n_layouts, P.n_nodes),
                                                      S.o, S.d, ta, cnt);
-        const int hb = Q.width_b == 4 ? trace4(Q.nodes_b, Q.prims_b, Q.prim_plane_b, Q.chain_b, Q.n_chain_b, Q.sphere_first_b,
-                                               Q.n_spheres_b, S.o, S.d, tb)
+        const int hb = Q.width_b == 4 ? trace4(Q.nodes_b, Q.prims_b, Q.chain_b, Q.n_chain_b, Q.sphere_first_b, Q.n_spheres_b,
+                                               S.o, S.d, tb)
                                       : trace<false>(Q.nodes_b, Q.prims_b, Q.n_nodes_b,
                                                      layout_base(S.d, Q.n_layouts_b, Q.n_nodes_b), S.o, S.d, tb, cnt);
         if (ha != hb) {
@@ -2117,7 +2104,6 @@ struct crt_scene {
     int sphere_first = 0, n_ray_spheres = 0;   // width 4: spheres tested per ray, prims [first, first + n)
     float sph2[2][12] = {};                    // width 4 with exactly two per-ray spheres: their kernel-argument copy
     int tree_spheres = 1;                      // width 4: some leaf holds a sphere
-    uint32_t prim_plane = 0;                   // width 4: primitives stored as 3 planes of float4 (prim_rec)
     long excluded = 0;
 };
 
@@ -2352,18 +2338,9 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
         return e;
     };
     const std::vector<int>& rc = rebuilt ? RB.rank_code : F.rank_code;
-    std::vector<float4> planes;                // width 4: the primitive records as three planes (prim_rec)
-    if (S->width == 4) {
-        const size_t n = RB.prims.size() / 3;
-        if (n * 48 >= ((size_t)1 << 32)) { crt_scene_destroy(S); return set_error(CRT_ERR_INVALID_ARGUMENT, "scene too large"); }
-        planes.resize(3 * n);
-        for (size_t p = 0; p < n; ++p)
-            for (int k = 0; k < 3; ++k) planes[k * n + p] = RB.prims[3 * p + k];
-        S->prim_plane = (uint32_t)(n * 16);
-    }
     hipError_t e;
     if ((e = up(&S->d_nodes, rebuilt ? RB.nodes : F.nodes)) != hipSuccess ||
-        (e = up(&S->d_prims, S->width == 4 ? planes : (rebuilt ? RB.prims : F.prims))) != hipSuccess ||
+        (e = up(&S->d_prims, rebuilt ? RB.prims : F.prims)) != hipSuccess ||
         (e = up(&S->d_mats, mats)) != hipSuccess ||
         (e = up(&S->d_chain, rebuilt ? RB.chain : std::vector<float4>())) != hipSuccess ||
         (e = up(&S->d_shade, shading_records(rc, rebuilt ? RB.prims : F.prims, D))) != hipSuccess) {
@@ -2551,7 +2528,6 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     RenderParams P{};
     P.nodes = S->d_nodes; P.prims = S->d_prims; P.mats = S->d_mats; P.shade = S->d_shade;
     P.n_nodes = S->n_nodes; P.n_mats = S->n_mats; P.n_prims = S->n_prims; P.n_layouts = S->layouts;
-    P.prim_plane = S->prim_plane;
     P.err = reinterpret_cast<unsigned*>(R->d_counters + ERR_WORD);
     P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
     P.accumulate = (flags & CRT_RENDER_ACCUMULATE) ? 1 : 0;
@@ -2750,13 +2726,11 @@ int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene*
     RenderParams& P = Q.A;
     P.nodes = A->d_nodes; P.prims = A->d_prims; P.mats = A->d_mats; P.shade = A->d_shade;
     P.n_nodes = A->n_nodes; P.n_mats = A->n_mats; P.n_prims = A->n_prims; P.n_layouts = A->layouts;
-    P.prim_plane = A->prim_plane;
     P.err = reinterpret_cast<unsigned*>(R->d_counters + ERR_WORD);
     P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
     P.accumulate = 0; P.regen_threshold = 64;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     Q.nodes_b = B->d_nodes; Q.prims_b = B->d_prims; Q.n_nodes_b = B->n_nodes; Q.n_layouts_b = B->layouts;
-    Q.prim_plane_b = B->prim_plane;
     Q.width_a = A->width; Q.width_b = B->width;
     Q.dump = nullptr;
     Q.max_dump = 0;

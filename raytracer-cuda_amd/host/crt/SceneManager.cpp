@@ -177,7 +177,7 @@ void SceneManager::loadObject(const std::string& filename, std::vector<MeshData>
 
 // createRandomWorld (CUDAKernels.h:28-84) + createBVH (:86-90)
 void SceneManager::createWorld() {
-    const int MAX_OBJECTS = 500, MAX_MATERIALS = 500;   // HittableList.cuh:328-329
+    const int MAX_OBJECTS = 500, MAX_MATERIALS = 500;   // HittableList.cuh:70-71
     m_Materials.clear(); m_Spheres.clear(); m_Objects.clear();
     auto addMaterial = [&](const crt_material_desc& m) -> int {
         if ((int)m_Materials.size() < MAX_MATERIALS) { m_Materials.push_back(m); return (int)m_Materials.size() - 1; }

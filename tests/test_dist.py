@@ -1,4 +1,4 @@
-"""spp sharding + framebuffer reduce, exercised on CPU with torch.distributed gloo (world 2).
+"""spp sharding + framebuffer reduce, exercised on CPU with torch.distributed gloo (worlds 2 and 4).
 
 The rank-local 'renderer' is the oracle (a stand-in for the HIP kernel, which needs a
 GPU); ShardedFrameRenderer, the shard plan and the collective are the production code.
@@ -52,14 +52,14 @@ class OracleShardRenderer:
         self.resolved = scale
 
 
-def _worker(rank, world, port, files, q):
+def _worker(rank, world, port, files, q, reduce_op="all_reduce"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import objload
     import pyoracle
     o = pyoracle.OracleScene(objload.load_scene(files))
     r = OracleShardRenderer(o, pyoracle.camera(), W, H)
-    fr = ShardedFrameRenderer(r, None, SPP, 20, 41, rank, world, reduce_op="all_reduce", fb_device="cpu")
+    fr = ShardedFrameRenderer(r, None, SPP, 20, 41, rank, world, reduce_op=reduce_op, fb_device="cpu")
     fr.render()
     q.put((rank, fr.spp, fr.subseq, fr.linear(), r.resolved))
     dist.destroy_process_group()
@@ -98,3 +98,31 @@ def test_gloo_world2_sharded_frame(scenes):
     assert not np.array_equal(s1, ref)      # different samples ...
     mean_diff = abs(float(s1.mean() - ref.mean())) / SPP
     assert mean_diff < 0.05                 # ... same estimator
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_reduce_to_rank0(scenes, world):
+    """reduce_op="reduce", the path bench.py runs on N GPUs (crt_amd/dist.py): rank 0 alone holds the reduced frame
+    (the rank-order sum of the shard renders, up to the collective's summation order) and resolves it with
+    1/spp_total; the other ranks never resolve."""
+    import objload
+    import pyoracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, scenes["cornell"], q, "reduce")) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in ps], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [shard_spp(SPP, world, k) for k in range(world)]
+    assert sum(r[1] for r in res) == SPP
+    assert [r[2] for r in res] == [k * W * H for k in range(world)]
+    o = pyoracle.OracleScene(objload.load_scene(scenes["cornell"]))
+    parts = [o.render(pyoracle.camera(), W, H, sp, 20, subseq_base=sb)[0] for (_, sp, sb, _, _) in res]
+    ref = reduce_framebuffers_cpu(parts)
+    assert np.allclose(res[0][3], ref, rtol=0, atol=1e-5)
+    assert res[0][4] == np.float32(1) / np.float32(SPP)          # rank 0: writeColor scale of the whole frame
+    assert all(r[4] is None for r in res[1:])                    # non-root ranks: no resolve

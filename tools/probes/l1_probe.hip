@@ -7,7 +7,7 @@
 // same binary gives the lookups (TCP_TOTAL_CACHE_ACCESSES) and cycles (GRBM_GUI_ACTIVE), so
 //   lookups per instruction  -> the L1 line size and how lookups count for each access shape;
 //   lookups per CU-cycle     -> the peak rate of the fully divergent shape (the render kernel's shape).
-// Shapes (64 lanes, 16 B each):
+// Shapes (64 lanes, 16 B each; the record shapes are in main()):
 //   coalesced : lane l reads bytes [16 l, 16 l + 16) of a 1 KiB row           (1 KiB contiguous per instruction)
 //   stride64  : lane l reads 16 B at 64 l                                      (4 KiB span, 2 lanes per 128-B line)
 //   stride128 : lane l reads 16 B at 128 l                                     (64 distinct 128-B lines)
@@ -59,18 +59,25 @@ __global__ __launch_bounds__(256) void l1_probe_kernel(const float4* __restrict_
     out[blockIdx.x * 256 + threadIdx.x] = acc.x + acc.y + acc.z + acc.w;
 }
 
-// 7 dwordx4 loads of one pseudo-random 128-B record per lane per iteration (the 4-wide node's box rows + meta)
-__global__ __launch_bounds__(256) void l1_probe_node128(const float4* __restrict__ table, float* __restrict__ out) {
+// R-row records of REC bytes, one pseudo-random record per lane per iteration, R dwordx4 loads per record.
+// ROT = 0: row k at byte 16 k of the record (every lane's load k at the same offset inside its line);
+// ROT = 1: row k at slot (k + record) mod (REC / 16) (the offset varies with the record);
+// ROT = 2: load k reads slot 0 of record (record + 37 k): random lines, every lane at offset 0.
+template <int REC, int R, int ROT>
+__global__ __launch_bounds__(256) void l1_probe_rec(const float4* __restrict__ table, float* __restrict__ out) {
     const float4* t = table + (blockIdx.x % 64) * TABLE_F4;
+    constexpr int SLOTS = REC / 16, NREC = TABLE_F4 / SLOTS;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     uint32_t h = hash(blockIdx.x * 256u + threadIdx.x);
 #pragma unroll 2
-    for (int i = 0; i < ITERS / 7; ++i) {
+    for (int i = 0; i < ITERS / R; ++i) {
         h = h * 1664525u + 1013904223u;
-        const float4* q = t + 8 * ((h >> 8) & (TABLE_F4 / 8 - 1));
+        const uint32_t rec = (h >> 8) & (NREC - 1);
+        const float4* q = t + SLOTS * rec;
 #pragma unroll
-        for (int k = 0; k < 7; ++k) {
-            const float4 v = q[k];
+        for (int k = 0; k < R; ++k) {
+            const uint32_t slot = ROT == 0 ? (uint32_t)k : ROT == 1 ? ((uint32_t)k + rec) & (SLOTS - 1) : 0u;
+            const float4 v = ROT == 2 ? t[SLOTS * ((rec + 37u * k) & (NREC - 1))] : q[slot];
             acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
         }
     }
@@ -91,18 +98,24 @@ int main() {
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
-    const char* names[5] = {"coalesced", "stride64", "stride128", "random", "node128"};
-    for (int s = 0; s < 5; ++s) {
+    struct Shape { const char* name; void (*k)(const float4*, float*); int per_iter; };
+    const Shape shapes[] = {
+        {"coalesced", l1_probe_kernel<0>, 1},
+        {"stride64", l1_probe_kernel<1>, 1},
+        {"stride128", l1_probe_kernel<2>, 1},
+        {"random", l1_probe_kernel<3>, 1},
+        {"node128", l1_probe_rec<128, 7, 0>, 7},          // the 4-wide node today: 7 rows at fixed offsets
+        {"node128_rot", l1_probe_rec<128, 7, 1>, 7},      // rows rotated by the record index
+        {"line128_slot0", l1_probe_rec<128, 7, 2>, 7},    // random lines, all lanes at offset 0
+        {"node64", l1_probe_rec<64, 4, 0>, 4},            // a 64-B node: 4 rows at fixed offsets
+        {"node64_rot", l1_probe_rec<64, 4, 1>, 4},
+        {"tri48", l1_probe_rec<64, 3, 0>, 3},             // 3 rows of a 64-B-aligned record (48-B triangle padded)
+    };
+    for (const Shape& sh : shapes) {
         float best = 1e30f;
         for (int rep = 0; rep < 3; ++rep) {
             CHECK(hipEventRecord(e0));
-            switch (s) {
-                case 0: hipLaunchKernelGGL((l1_probe_kernel<0>), dim3(blocks), dim3(256), 0, 0, d_table, d_out); break;
-                case 1: hipLaunchKernelGGL((l1_probe_kernel<1>), dim3(blocks), dim3(256), 0, 0, d_table, d_out); break;
-                case 2: hipLaunchKernelGGL((l1_probe_kernel<2>), dim3(blocks), dim3(256), 0, 0, d_table, d_out); break;
-                case 3: hipLaunchKernelGGL((l1_probe_kernel<3>), dim3(blocks), dim3(256), 0, 0, d_table, d_out); break;
-                default: hipLaunchKernelGGL(l1_probe_node128, dim3(blocks), dim3(256), 0, 0, d_table, d_out); break;
-            }
+            hipLaunchKernelGGL(sh.k, dim3(blocks), dim3(256), 0, 0, d_table, d_out);
             CHECK(hipGetLastError());
             CHECK(hipEventRecord(e1));
             CHECK(hipEventSynchronize(e1));
@@ -110,10 +123,10 @@ int main() {
             CHECK(hipEventElapsedTime(&ms, e0, e1));
             if (ms < best) best = ms;
         }
-        const double insts = (double)blocks * 4 * (s == 4 ? (ITERS / 7) * 7 : ITERS);   // wave-level load insts
+        const double insts = (double)blocks * 4 * (ITERS / sh.per_iter) * sh.per_iter;   // wave-level load insts
         std::printf("{\"shape\": \"%s\", \"cus\": %d, \"blocks\": %d, \"wave_load_insts\": %.0f, \"best_ms\": %.4f, "
-                    "\"insts_per_cu_per_ns\": %.5f}\n",
-                    names[s], cus, blocks, insts, best, insts / cus / (best * 1e6));
+                    "\"cycles_per_inst_at_2p4GHz\": %.2f}\n",
+                    sh.name, cus, blocks, insts, best, best * 1e6 * 2.4 / (insts / cus));
     }
     CHECK(hipFree(d_table));
     CHECK(hipFree(d_out));
