@@ -558,8 +558,17 @@ __device__ __forceinline__ V3 sphere_inv(V3 d, V3 binv) {
         return v3(recip_exact_any(d.x), recip_exact_any(d.y), recip_exact_any(d.z));
     return binv;
 }
-__device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ q, V3 o, V3 inv, float tmax) {
-    const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
+// Row k of 4-wide node n sits at 16-B slot k ^ (n & 7) of the node's 128-B record (swizzled at upload,
+// crt_scene_create_ex).  One wave instruction loads row k of up to 64 different nodes; at a fixed slot every lane reads
+// the same 16-B offset of its line, and the vector L1 then serves about one lane per cycle (tools/probes/l1_probe,
+// profiles/r02c: 62 cycles per instruction for that shape against 38 for random offsets).  b = node_base(n).
+__device__ __forceinline__ uint32_t node_base(int node) { return ((uint32_t)node << 7) | (((uint32_t)node & 7u) << 4); }
+__device__ __forceinline__ float4 node_row(const float4* __restrict__ nodes, uint32_t b, uint32_t k) {
+    return *rec_at(nodes, b ^ (k << 4));
+}
+__device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ nodes, uint32_t b, V3 o, V3 inv, float tmax) {
+    const float4 lx = node_row(nodes, b, 0), hx = node_row(nodes, b, 1), ly = node_row(nodes, b, 2);
+    const float4 hy = node_row(nodes, b, 3), lz = node_row(nodes, b, 4), hz = node_row(nodes, b, 5);
     const pf2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
     const float nx = -(o.x * inv.x), ny = -(o.y * inv.y), nz = -(o.z * inv.z);
     const pf2 ox = {nx, nx}, oy = {ny, ny}, oz = {nz, nz};
@@ -698,9 +707,9 @@ __device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict
     ray_spheres(prims, chain, n_chain, sphere_first, n_spheres, o, d, inv, closest, hit);
     int stack[64];
     while (node >= 0) {
-        const float4* q = nodes + 8 * (size_t)node;
-        const Wide4 w = wide_boxes(q, o, box_inv(inv), closest);
-        const float4 mf = q[6];
+        const uint32_t b = node_base(node);
+        const Wide4 w = wide_boxes(nodes, b, o, box_inv(inv), closest);
+        const float4 mf = node_row(nodes, b, 6);
         const int first_child = __float_as_int(mf.x), n_int = __float_as_int(mf.y) & 0xff;
         const uint32_t counts = __float_as_uint(mf.w);
         int off = 0;
@@ -760,9 +769,9 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
     leaf_n = 0;
     leaf_first = 0;
     if (node >= 0) {
-        const float4* q = rec_at(P.nodes, (uint32_t)node << 7);
-        const float4 mf = q[6];
-        const Wide4 w = wide_boxes(q, o, inv, closest);
+        const uint32_t b = node_base(node);
+        const float4 mf = node_row(P.nodes, b, 6);
+        const Wide4 w = wide_boxes(P.nodes, b, o, inv, closest);
         // keep the whole link row in the node's loads: left to itself the compiler loads leaf_first / counts
         // only inside the leaf branch, one more dependent load on a leaf step's critical path.  Pinned after the
         // box tests, so the wait it implies is the one the boxes need anyway (pinned before them, it made the six
@@ -2338,8 +2347,14 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
         return e;
     };
     const std::vector<int>& rc = rebuilt ? RB.rank_code : F.rank_code;
+    std::vector<float4> swizzled;   // width 4: row k of node n at slot k ^ (n & 7) of its record (node_row)
+    if (S->width == 4) {
+        swizzled.resize(RB.nodes.size());
+        for (size_t n = 0; n < RB.nodes.size() / 8; ++n)
+            for (size_t k = 0; k < 8; ++k) swizzled[8 * n + (k ^ (n & 7))] = RB.nodes[8 * n + k];
+    }
     hipError_t e;
-    if ((e = up(&S->d_nodes, rebuilt ? RB.nodes : F.nodes)) != hipSuccess ||
+    if ((e = up(&S->d_nodes, S->width == 4 ? swizzled : (rebuilt ? RB.nodes : F.nodes))) != hipSuccess ||
         (e = up(&S->d_prims, rebuilt ? RB.prims : F.prims)) != hipSuccess ||
         (e = up(&S->d_mats, mats)) != hipSuccess ||
         (e = up(&S->d_chain, rebuilt ? RB.chain : std::vector<float4>())) != hipSuccess ||
