@@ -58,7 +58,6 @@ def workload_name(args) -> str:
     k = BASELINE_CONFIGS.get((args.scene, args.width, args.height, args.spp, args.bounces))
     return w + (f" (configs[{k}])" if k is not None else "")
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
-VALU_PEAK_TOPS = 157.3 / 2       # f32 vector: 157.3 TFLOP/s counts an FMA as 2; the path has no FMA
 
 # Algorithmic bytes / FP ops per unit of work:
 B_BOX, B_TRI, B_SPHERE, B_RAY = 32, 36, 20, 16     # node box+link; v0,e1,e2; c,r,r^2; material/hit
@@ -95,6 +94,8 @@ def parse():
     ap.add_argument("--leaf-size", type=int, default=4)
     ap.add_argument("--traversal-cost", type=float, default=2.0)
     ap.add_argument("--no-parity", action="store_true", help="skip the reference-BVH parity frame")
+    ap.add_argument("--print-workload-key", action="store_true",
+                    help="print the key of profiles/roofline_counters.json for these arguments and exit (tools/pmc.sh)")
     ap.add_argument("--host-build", action="store_true",
                     help="build the BVHs on the host (mesh: the sequential restatement of the reference builder; "
                          "rebuilt tree: crt_sah.h) instead of on the GPU")
@@ -158,21 +159,67 @@ def cpu_baseline(args, cam_floats, log_fn):
             "frame_wall_s" if full else "frame_wall_s_extrapolated": round(dt * args.spp / spp, 3)}
 
 
-def pmc_traffic(workload_key: str):
-    """HBM bytes per render launch from a committed rocprofv3 --pmc summary for this workload (or None)."""
-    p = REPO / "profiles" / "pmc_traffic.json"
+def workload_key(args, spp: int) -> str:
+    return (f"{args.scene}_{args.width}x{args.height}_{spp}spp_{args.bounces}b"
+            + ("" if args.bvh == "reference" else f"_rebuilt{args.bvh_width}"))
+
+
+def kernel_source_sha() -> str:
+    import hashlib
+    return hashlib.sha256((REPO / "raytracer-cuda_amd" / "csrc" / "crt_hip.hip").read_bytes()).hexdigest()
+
+
+def roofline_counters(key: str, kname: str):
+    """The committed PMC summary of this workload (tools/pmc_summary.py), if its kernel matches."""
+    p = REPO / "profiles" / "roofline_counters.json"
     if not p.exists():
-        return None, None
-    try:
-        d = json.loads(p.read_text())
-        e = d.get(workload_key)
-        return (e["hbm_bytes_per_launch"], e.get("source")) if e else (None, None)
-    except Exception:
-        return None, None
+        return None
+    e = json.loads(p.read_text()).get(key)
+    return e if e and e.get("kernel") == kname else None
+
+
+def roofline_from_counters(e, rays: int, kernel_s: float):
+    """Utilisation of the units that can bind the render kernel, from the per-ray counter values of the committed
+    PMC run (same workload, same kernel) scaled by THIS run's exact ray count and HIP-event kernel time.  The bound is
+    the unit with the largest fraction of its peak (MI355X_MICROARCH.md chip table: 1024 SIMDs at 2.4 GHz, a wave64
+    VALU instruction per 2 SIMD cycles; vector-L1 peak from the calibration probe; HBM 8 TB/s)."""
+    pr, d = e["per_ray"], e["derived"]
+    clk = 2.4e9
+    units = {}
+    valu = pr["SQ_INSTS_VALU"] * rays / kernel_s * 64 / 1e12          # issued lane-ops per second
+    valu_peak = 1024 * clk / 2 * 64 / 1e12                             # 78.6 TOP/s (= 157.3 TFLOP/s FMA-counted / 2)
+    units["valu"] = {"achieved": round(valu, 3), "peak": round(valu_peak, 2), "unit": "TOP/s (issued lane-ops)",
+                     "frac": round(valu / valu_peak, 4), "lane_util": d.get("valu_lane_util"),
+                     "useful_TOP_s": round(valu * d.get("valu_lane_util", 1.0), 3)}
+    if "TCP_TOTAL_CACHE_ACCESSES" in pr and "vl1_calibration" in e:
+        acc = pr["TCP_TOTAL_CACHE_ACCESSES"] * rays / kernel_s / 1e12
+        cal = e["vl1_calibration"]
+        peak = 256 * clk * cal["peak_accesses_per_cu_cycle"] / 1e12
+        units["vl1"] = {"achieved": round(acc, 4), "peak": round(peak, 4), "unit": "T accesses/s (TCP_TOTAL_CACHE_ACCESSES)",
+                        "frac": round(acc / peak, 4), "peak_shape": cal["peak_shape"],
+                        "note": "peak = the fastest access shape of tools/probes/l1_probe.hip; fixed-offset divergent "
+                                "16-B gathers run at "
+                                + str(min(cal["all"].values())) + " accesses per CU-cycle"}
+    if "hbm_bytes_per_launch" in d:
+        hbm = d["hbm_bytes_per_launch"] / e["rays_per_launch"] * rays / kernel_s / 1e9
+        units["hbm"] = {"achieved": round(hbm, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(hbm / HBM_PEAK_GBS, 5)}
+    bound = max(units, key=lambda k: units[k]["frac"])
+    u = units[bound]
+    traffic = (d["hbm_bytes_per_launch"] / e["rays_per_launch"] * rays) if "hbm_bytes_per_launch" in d else None
+    return {"bound": bound, "achieved": u["achieved"], "peak": u["peak"], "unit": u["unit"], "frac": u["frac"],
+            "traffic": int(traffic) if traffic else None, "units": units,
+            "counters": {k: d[k] for k in ("valu_busy", "valu_lane_util", "tcp_accesses_per_cu_cycle",
+                                           "tcp_pending_stall_frac", "wave_frac_waiting_memory", "l2_hit_rate")
+                         if k in d},
+            "counters_source": e["source"], "counters_clock_ghz": e["clock_ghz"],
+            "counters_kernel_source_current": e.get("kernel_source_sha256") == kernel_source_sha()}
 
 
 def main():
     args = parse()
+    if args.print_workload_key:
+        print(workload_key(args, args.spp))
+        return
     import torch
     import torch.distributed as dist
 
@@ -274,7 +321,7 @@ def main():
             f.write(img[::-1, :, :3].tobytes())
 
     # exact work counts for the same launch (deterministic: same seed, same shard)
-    roofline = roofline_valu = None
+    roofline = algorithmic = None
     work = None
     if not args.no_count:
         r.init_rand(args.seed, fr.subseq)
@@ -287,28 +334,28 @@ def main():
     except (IndexError, ValueError):
         variant = args.kernel_variant
     if work is not None:
+        # algorithmic bytes / ops of SURVEY §8(d), counted exactly by the COUNT kernel: served by L1/L2/MALL (the scene
+        # is cache-resident), so they are reported as a rate, never as a fraction of HBM
         bytes_launch = (B_BOX * work["box_tests"] + B_TRI * work["tri_tests"] + B_SPHERE * work["sphere_tests"]
                         + B_RAY * work["rays"] + B_PIXEL * W * H)
         flops_launch = (F_BOX * work["box_tests"] + F_TRI * work["tri_tests"] + F_SPHERE * work["sphere_tests"]
                         + F_RAY * work["rays"])
-        achieved = bytes_launch / (kernel_ms_avg / 1e3) / 1e9
-        wkey = f"{args.scene}_{W}x{H}_{fr.spp}spp_{args.bounces}b" + ("" if args.bvh == "reference" else
-                                                                      f"_rebuilt{args.bvh_width}")
-        traffic, tsrc = pmc_traffic(wkey)
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "bytes_per_launch": int(bytes_launch), "kernel": kname,
-                    "kernel_ms_avg": round(kernel_ms_avg, 3),
-                    "per_ray": {"box_tests": round(work["box_tests"] / work["rays"], 3),
-                                "tri_tests": round(work["tri_tests"] / work["rays"], 3),
-                                "sphere_tests": round(work["sphere_tests"] / work["rays"], 3)},
-                    "note": "algorithmic bytes = 32*box + 36*tri + 20*sphere + 16*ray + 60*pixel (DESIGN.md); "
-                            "the scene (%.1f MB) is L2/Infinity-Cache resident, so HBM traffic is far below "
-                            "this" % (st["device_bytes"] / 1e6)
-                            + ("" if traffic is None else f"; traffic from {tsrc}")}
-        valu = flops_launch / (kernel_ms_avg / 1e3) / 1e12
-        roofline_valu = {"bound": "valu", "achieved": round(valu, 2), "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
-                         "frac": round(valu / VALU_PEAK_TOPS, 4), "ops_per_launch": int(flops_launch)}
+        algorithmic = {"bytes_per_launch": int(bytes_launch),
+                       "cache_served_GB_s": round(bytes_launch / (kernel_ms_avg / 1e3) / 1e9, 1),
+                       "ops_per_launch": int(flops_launch),
+                       "ops_TOP_s": round(flops_launch / (kernel_ms_avg / 1e3) / 1e12, 3),
+                       "per_ray": {"box_tests": round(work["box_tests"] / work["rays"], 3),
+                                   "tri_tests": round(work["tri_tests"] / work["rays"], 3),
+                                   "sphere_tests": round(work["sphere_tests"] / work["rays"], 3)},
+                       "note": "32*box + 36*tri + 20*sphere + 16*ray + 60*pixel bytes; 24*box + 54*tri + 30*sphere "
+                               "+ 100*ray f32 ops (DESIGN.md §5); the %.1f MB scene is L2/Infinity-Cache resident"
+                               % (st["device_bytes"] / 1e6)}
+    ec = roofline_counters(workload_key(args, fr.spp), kname)
+    if ec is not None:
+        roofline = roofline_from_counters(ec, rays_rank, kernel_ms_avg / 1e3)
+        roofline.update(kernel=kname, kernel_ms_avg=round(kernel_ms_avg, 3))
+    else:
+        log_r(f"[roofline] no committed counter summary for {workload_key(args, fr.spp)} / {kname}: roofline null")
 
     # parity of the timed configuration against the reference's own BVH on the same frame (N=1)
     parity = None
@@ -362,7 +409,7 @@ def main():
             "rays_per_frame": rays_frame,
             "paths_per_s": round(W * H * args.spp * args.steps / elapsed, 1),
             "render_kernel_ms_avg": round(kernel_ms_avg, 3), "render_kernel_ms_max_over_ranks": round(kernel_ms_max, 3),
-            "roofline": roofline, "roofline_valu": roofline_valu, "cpu_baseline": cpu, "parity": parity,
+            "roofline": roofline, "algorithmic": algorithmic, "cpu_baseline": cpu, "parity": parity,
             "setup": setup,
         }
         print(json.dumps(out), flush=True)
