@@ -13,6 +13,9 @@ namespace CRT {
 static inline bool is_digit(char c) { return c >= '0' && c <= '9'; }
 static inline bool is_space(char c) { return c == ' ' || c == '\t'; }
 
+// Number parser following tinyobjloader v1.0's tryParseDouble (the reference's OBJ dependency; tinyobjloader is
+// MIT-licensed, Copyright (c) 2012-2016 Syoyo Fujita and many contributors), restated so that vertex coordinates round
+// exactly as the reference's loader rounds them.
 bool TryParseDouble(const char* s, const char* s_end, double* result) {
     if (s >= s_end) return false;
     double mantissa = 0.0;
