@@ -236,6 +236,11 @@ int  crt_renderer_set_schedule(crt_renderer* r, int probe_spp, int min_spp, int 
 /* Variants 2-4, 7, 8: number of parked lanes (1..64) that triggers a shading/regeneration pass; default 24 for
  * variants 2/3 and 44 for the 4-wide variants (setting it sets both). */
 int  crt_renderer_set_regen_threshold(crt_renderer* r, int lanes);
+/* Variant 8 with the cost probe: the first `tiles` tiles of the cost order (the most expensive; -1 = automatic, 4 per
+ * CU, the default) trigger their shading/regeneration passes at `lanes` parked lanes (default 16) instead of the
+ * regeneration threshold.  A frame with few tiles per wave slot ends with its most expensive tile, whose pixels' sample
+ * chains are sequential; waiting less for the wave's other lanes shortens that chain.  Results never depend on it. */
+int  crt_renderer_set_critical_tiles(crt_renderer* r, int tiles, int lanes);
 /* Variant 4: per-lane traversal-stack entries kept in LDS (1..16, default 16); deeper entries spill to a
  * per-pixel region in HBM.  Results do not depend on it (tests force the HBM path with 1). */
 int  crt_renderer_set_stack_lds(crt_renderer* r, int entries);

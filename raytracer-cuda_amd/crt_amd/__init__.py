@@ -218,6 +218,9 @@ class Renderer:
         flags = (int(tile_key) & 0xf) << 16
         check(_lib.hip().crt_renderer_set_schedule(self.h, int(probe_spp), int(min_spp), flags), "set_schedule")
 
+    def set_critical_tiles(self, tiles: int = -1, lanes: int = 16):
+        check(_lib.hip().crt_renderer_set_critical_tiles(self.h, int(tiles), int(lanes)), "set_critical_tiles")
+
     def set_kernel_variant(self, variant: int):
         check(_lib.hip().crt_renderer_set_kernel_variant(self.h, int(variant)), "set_kernel_variant")
 

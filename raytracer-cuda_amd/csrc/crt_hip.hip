@@ -73,6 +73,8 @@ struct RenderParams {
     int n_slots;
     int tiles_x;                          // variant 8: 8x8 tiles per row (order[] holds tile indices)
     uint32_t* __restrict__ probe_cost;    // probe launch (variant 4): rays per pixel; nothing else is written
+    int crit_tiles, crit_threshold;       // variant 8: the first crit_tiles tiles of the cost order regenerate at
+                                          // crit_threshold parked lanes instead of regen_threshold
 };
 
 struct TraceCounts {
@@ -1211,13 +1213,16 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         float closest = INF;
         V3 inv = v3(0.f, 0.f, 0.f);
         L.owner_at[lane] = 0;      // traverse_step4: owner + 1, 0 = none
+        // variant 8: the most expensive tiles of the cost order bound the frame when it has few tiles per wave slot
+        // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
+        const int regen_t = (TILED && (int)blockIdx.x < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
         for (;;) {
             const bool parked = live && node < 0;
             const int n_parked = __popcll(__ballot(parked));
             const int n_live = __popcll(__ballot(live));
             if (n_live == 0) break;
             const uint64_t c0 = COUNT ? shader_clock() : 0;
-            if (n_parked >= P.regen_threshold || n_parked == n_live) {
+            if (n_parked >= regen_t || n_parked == n_live) {
                 if (COUNT) cnt.passes++;
                 if (parked) {
                     const uint64_t s0 = COUNT ? shader_clock() : 0;
@@ -2150,6 +2155,8 @@ struct crt_renderer {
     unsigned long long prof[7] = {0, 0, 0, 0, 0, 0, 0};   // COUNT-mode section profile (variant 4)
     int regen_threshold = 24;      // variants 2/3
     int regen_threshold_wide = 44; // variants 4/7/8 (measured: 40 for variant 4, profiles/r01d; 44-48 for 8, r01af)
+    int crit_tiles = -1;           // variant 8: leading tiles of the cost order regenerating at crit_threshold; -1 = 4 per CU
+    int crit_threshold = 16;       // (measured: profiles/r02h, r02i)
     int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 6 for 4-wide scenes, 5 otherwise
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
     size_t ovf_entries = 0;
@@ -2500,6 +2507,13 @@ int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int f
     return CRT_OK;
 }
 
+int crt_renderer_set_critical_tiles(crt_renderer* R, int tiles, int lanes) {
+    if (!R || tiles < -1 || lanes < 1 || lanes > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "critical tiles >= -1, lanes 1..64");
+    R->crit_tiles = tiles;
+    R->crit_threshold = lanes;
+    return CRT_OK;
+}
+
 int crt_renderer_set_occupancy_target(crt_renderer* R, int waves_per_simd) {
     if (!R || waves_per_simd < 0 || waves_per_simd > 8) return set_error(CRT_ERR_INVALID_ARGUMENT, "waves per SIMD 0..8");
     R->min_waves = waves_per_simd;
@@ -2548,7 +2562,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.accumulate = (flags & CRT_RENDER_ACCUMULATE) ? 1 : 0;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     P.ovf = nullptr;
-    P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0;
+    P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0; P.crit_tiles = 0; P.crit_threshold = 64;
     P.stack_cap = S->stack_cap;
     P.sphere_first = S->sphere_first;
     P.n_ray_spheres = S->n_ray_spheres;
@@ -2626,6 +2640,8 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             hipLaunchKernelGGL(crt_order_scatter_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key, n_tiles,
                                R->d_order_hist, R->d_order, 0u);
             P.order = R->d_order;
+            P.crit_tiles = R->crit_tiles < 0 ? 4 * R->n_cus : R->crit_tiles;
+            P.crit_threshold = R->crit_threshold;
         }
         const dim3 tgrid(n_tiles), tblock(64);
         const char* cs = cnt ? "true" : "false";

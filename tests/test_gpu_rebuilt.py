@@ -193,7 +193,21 @@ def test_tile_key_modes_are_bit_identical(rebuilt, key):
     _schedule_case(rebuilt, 8, 4, tile_key=key)
 
 
-def _schedule_case(rebuilt, variant, probe_spp, **flags):
+@pytest.mark.parametrize("tiles,lanes", [(0, 16), (10, 1), (-1, 64), (1000000, 5)])
+def test_critical_tiles_are_bit_identical(rebuilt, tiles, lanes):
+    """Variant 8's critical tiles (the leading tiles of the cost order regenerate at fewer parked lanes): none, the
+    first 10 at every parked lane, the automatic count, every tile."""
+    _schedule_case(rebuilt, 8, 4, crit=(tiles, lanes))
+
+
+def test_critical_tiles_rejects_bad_arguments():
+    r = crt_amd.Renderer(16, 16)
+    for tiles, lanes in ((-2, 16), (0, 0), (0, 65)):
+        with pytest.raises(crt_amd.CrtError):
+            r.set_critical_tiles(tiles, lanes)
+
+
+def _schedule_case(rebuilt, variant, probe_spp, crit=None, **flags):
     """A schedule option, with and without the cost probe: the same frame and RNG state as variant 4."""
     dev = rebuilt["cornell_bunny", "w4"]
     w, h, spp = 104, 45, 64          # 13 x 6 = 78 tiles, the last row partial
@@ -202,6 +216,8 @@ def _schedule_case(rebuilt, variant, probe_spp, **flags):
     b = crt_amd.Renderer(w, h)
     b.set_kernel_variant(variant)
     b.set_schedule(probe_spp, 64, **flags)
+    if crit is not None:
+        b.set_critical_tiles(*crit)
     b.set_camera(cam)
     b.init_rand(41)
     b.render(dev, spp, 20)

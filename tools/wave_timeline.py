@@ -38,7 +38,8 @@ r.init_rand(41)
 r.render(sc, a.spp, 20)
 r.synchronize()
 kernel_ms = r.last_kernel_ms()
-n_waves = ((a.w + 15) // 16) * ((a.h + 15) // 16) * 4 if a.variant not in (7, 8) else a.persistent_waves
+n_waves = (((a.w + 7) // 8) * ((a.h + 7) // 8) if a.variant == 8 else
+           a.persistent_waves if a.variant == 7 else ((a.w + 15) // 16) * ((a.h + 15) // 16) * 4)
 L = _lib.hip()
 L.crt_profile_wave_times.argtypes = [C.c_void_p, C.c_int]
 buf = np.zeros((n_waves, 2), np.uint64)
