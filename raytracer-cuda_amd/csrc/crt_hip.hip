@@ -568,26 +568,34 @@ __device__ __forceinline__ uint32_t node_base(int node) { return ((uint32_t)node
 __device__ __forceinline__ float4 node_row(const float4* __restrict__ nodes, uint32_t b, uint32_t k) {
     return *rec_at(nodes, b ^ (k << 4));
 }
+// The slab test by the ray's direction signs: for axis a, the row of the four child planes the ray enters first (lo
+// for inv >= 0, hi for inv < 0) is row 2a ^ sign_a, and the row it leaves by is the other one.  fma(plane, inv, -o*inv)
+// is monotone in the plane, so the entry row's t values are exactly min(t_lo, t_hi) and the exit row's exactly
+// max(t_lo, t_hi): the same box hits and tmin as the min/max form, bit for bit, without its 24 min/max per node.  The
+// row choice is an address bit (the sign of inv, shifted to the row's 16-B slot), not a select.
+__device__ __forceinline__ uint32_t sign_row(float inv) { return (__float_as_uint(inv) >> 27) & 16u; }
 __device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ nodes, uint32_t b, V3 o, V3 inv, float tmax) {
-    const float4 lx = node_row(nodes, b, 0), hx = node_row(nodes, b, 1), ly = node_row(nodes, b, 2);
-    const float4 hy = node_row(nodes, b, 3), lz = node_row(nodes, b, 4), hz = node_row(nodes, b, 5);
+    const uint32_t sx = sign_row(inv.x), sy = sign_row(inv.y), sz = sign_row(inv.z);
+    const float4 nxr = *rec_at(nodes, b ^ sx), fxr = *rec_at(nodes, b ^ (16u ^ sx));
+    const float4 nyr = *rec_at(nodes, b ^ (32u ^ sy)), fyr = *rec_at(nodes, b ^ (48u ^ sy));
+    const float4 nzr = *rec_at(nodes, b ^ (64u ^ sz)), fzr = *rec_at(nodes, b ^ (80u ^ sz));
     const pf2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
     const float nx = -(o.x * inv.x), ny = -(o.y * inv.y), nz = -(o.z * inv.z);
     const pf2 ox = {nx, nx}, oy = {ny, ny}, oz = {nz, nz};
-    const pf2 ax0 = __builtin_elementwise_fma((pf2){lx.x, lx.y}, ix, ox), ax1 = __builtin_elementwise_fma((pf2){lx.z, lx.w}, ix, ox);
-    const pf2 bx0 = __builtin_elementwise_fma((pf2){hx.x, hx.y}, ix, ox), bx1 = __builtin_elementwise_fma((pf2){hx.z, hx.w}, ix, ox);
-    const pf2 ay0 = __builtin_elementwise_fma((pf2){ly.x, ly.y}, iy, oy), ay1 = __builtin_elementwise_fma((pf2){ly.z, ly.w}, iy, oy);
-    const pf2 by0 = __builtin_elementwise_fma((pf2){hy.x, hy.y}, iy, oy), by1 = __builtin_elementwise_fma((pf2){hy.z, hy.w}, iy, oy);
-    const pf2 az0 = __builtin_elementwise_fma((pf2){lz.x, lz.y}, iz, oz), az1 = __builtin_elementwise_fma((pf2){lz.z, lz.w}, iz, oz);
-    const pf2 bz0 = __builtin_elementwise_fma((pf2){hz.x, hz.y}, iz, oz), bz1 = __builtin_elementwise_fma((pf2){hz.z, hz.w}, iz, oz);
+    const pf2 ax0 = __builtin_elementwise_fma((pf2){nxr.x, nxr.y}, ix, ox), ax1 = __builtin_elementwise_fma((pf2){nxr.z, nxr.w}, ix, ox);
+    const pf2 bx0 = __builtin_elementwise_fma((pf2){fxr.x, fxr.y}, ix, ox), bx1 = __builtin_elementwise_fma((pf2){fxr.z, fxr.w}, ix, ox);
+    const pf2 ay0 = __builtin_elementwise_fma((pf2){nyr.x, nyr.y}, iy, oy), ay1 = __builtin_elementwise_fma((pf2){nyr.z, nyr.w}, iy, oy);
+    const pf2 by0 = __builtin_elementwise_fma((pf2){fyr.x, fyr.y}, iy, oy), by1 = __builtin_elementwise_fma((pf2){fyr.z, fyr.w}, iy, oy);
+    const pf2 az0 = __builtin_elementwise_fma((pf2){nzr.x, nzr.y}, iz, oz), az1 = __builtin_elementwise_fma((pf2){nzr.z, nzr.w}, iz, oz);
+    const pf2 bz0 = __builtin_elementwise_fma((pf2){fzr.x, fzr.y}, iz, oz), bz1 = __builtin_elementwise_fma((pf2){fzr.z, fzr.w}, iz, oz);
     const float ax[4] = {ax0.x, ax0.y, ax1.x, ax1.y}, bx[4] = {bx0.x, bx0.y, bx1.x, bx1.y};
     const float ay[4] = {ay0.x, ay0.y, ay1.x, ay1.y}, by[4] = {by0.x, by0.y, by1.x, by1.y};
     const float az[4] = {az0.x, az0.y, az1.x, az1.y}, bz[4] = {bz0.x, bz0.y, bz1.x, bz1.y};
     Wide4 w;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        const float t0 = fmaxf(fmaxf(fminf(ax[s], bx[s]), fminf(ay[s], by[s])), fmaxf(fminf(az[s], bz[s]), 0.001f));
-        const float t1 = fminf(fminf(fmaxf(ax[s], bx[s]), fmaxf(ay[s], by[s])), fminf(fmaxf(az[s], bz[s]), tmax));
+        const float t0 = fmaxf(fmaxf(ax[s], ay[s]), fmaxf(az[s], 0.001f));
+        const float t1 = fminf(fminf(bx[s], by[s]), fminf(bz[s], tmax));
         w.tmin[s] = t0;
         w.hit[s] = t0 < t1;
     }
