@@ -213,6 +213,8 @@ void crt_renderer_destroy(crt_renderer* r);
 /* curand_init(seed, subsequence_base + y*width + x, 0) per pixel (CUDAKernels.h:18-26).
  * subsequence_base = shard * width * height for spp sharding. */
 int  crt_renderer_init_rand(crt_renderer* r, unsigned long long seed, unsigned long long subsequence_base, void* stream);
+/* CRT_ERR_INVALID_ARGUMENT for a non-finite origin or lens radius, or |origin| >= 2^59 / lens_radius >= 2^58 (the
+ * rebuilt tree's slab test needs |o| * 2^64 finite; every real scene is many orders of magnitude inside it). */
 int  crt_renderer_set_camera(crt_renderer* r, const crt_camera_desc* cam);
 /* Render-kernel variant (identical results, different wave scheduling).  Scenes with threaded binary nodes
  * (CRT_BVH_REFERENCE, or REBUILT width 2; default 3): 0 = per-lane BVH traversal with per-lane leaf loops; 1 = per-lane

@@ -546,7 +546,8 @@ struct Wide4 {
 // lo * inv - o * inv = inf - inf = NaN on a plane, and the min/max would then cull a box the ray runs inside of.
 // The traversal's 1/d is therefore the exact 1/d clamped to +-2^64 (box_inv): a plane keeps its sign and a magnitude
 // >= padding * 2^64, far above the rounding, and |coord| * 2^64 stays finite for every |coord| < 2^60, the bound
-// crt_scene_create_ex enforces on the rebuilt tree's boxes and render() on the camera origin.
+// crt_scene_create_ex enforces on the rebuilt tree's boxes (every later ray origin is a hit point inside them) and
+// crt_renderer_set_camera on the primary rays' origins (camera origin + lens offset, below 2^59 + 2^58).
 constexpr float BOX_INV_CLAMP = 0x1p64f;
 __device__ __forceinline__ V3 box_inv(V3 inv) {
     return v3(__builtin_amdgcn_fmed3f(inv.x, -BOX_INV_CLAMP, BOX_INV_CLAMP),
@@ -2543,6 +2544,11 @@ int crt_renderer_set_regen_threshold(crt_renderer* R, int lanes) {
 
 int crt_renderer_set_camera(crt_renderer* R, const crt_camera_desc* cam) {
     if (!R || !cam) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    // primary rays start within lens_radius of the origin (right/up are unit vectors); the 4-wide slab test needs
+    // |o| * 2^64 finite (box_inv), the same 2^60 bound the rebuilt tree's boxes are held to
+    bool ok = std::isfinite(cam->lens_radius) && std::fabs(cam->lens_radius) < 0x1p58f;
+    for (int a = 0; a < 3; ++a) ok = ok && std::isfinite(cam->origin[a]) && std::fabs(cam->origin[a]) < 0x1p59f;
+    if (!ok) return set_error(CRT_ERR_INVALID_ARGUMENT, "camera origin or lens radius non-finite or beyond 2^59");
     R->cam = *cam;
     R->has_camera = true;
     return CRT_OK;

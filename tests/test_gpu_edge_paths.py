@@ -240,3 +240,20 @@ def test_stack_overflow_reported_through_hiprenderer(scenes):
     ok = crt_amd.Viewer(scenes["cornell_bunny"], 96, 54, bvh="rebuilt", bvh_width=4, pos=(0.0, 0.0, 0.3), focus=0.3)
     ok.renderer.set_stack_lds(1)
     assert ok.frame()["frame"] == 1
+
+
+def test_camera_beyond_slab_bound_rejected():
+    """crt_renderer_set_camera refuses an origin the 4-wide slab test cannot take (|o| * 2^64 must stay finite,
+    crt_hip.hip box_inv) instead of rendering a frame whose box tests produce NaN."""
+    r = crt_amd.Renderer(8, 8)
+    cam = crt_amd.camera(1)
+    r.set_camera(cam)
+    for bad in (float("inf"), float("nan"), 2.0 ** 62):
+        c = crt_amd.camera(1)
+        c.origin[1] = bad
+        with pytest.raises(crt_amd.CrtError, match="beyond 2\\^59"):
+            r.set_camera(c)
+    c = crt_amd.camera(1)
+    c.lens_radius = float("inf")
+    with pytest.raises(crt_amd.CrtError, match="beyond 2\\^59"):
+        r.set_camera(c)
