@@ -89,8 +89,15 @@ def parse():
     ap.add_argument("--save-ppm", default="", help="rank 0 writes the resolved frame here")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--kernel-variant", type=int, default=None, help="render-kernel variant (default: library's)")
+    ap.add_argument("--regen-threshold", type=int, default=None,
+                    help="parked lanes before a regeneration pass (default: the library's, 44 for 4-wide scenes)")
+    ap.add_argument("--critical-tiles", type=int, default=None,
+                    help="variant 8: leading tiles of the cost order that regenerate sooner (default: library's)")
+    ap.add_argument("--critical-lanes", type=int, default=16, help="their regeneration threshold")
     ap.add_argument("--bvh", default="rebuilt", choices=["rebuilt", "reference"])
     ap.add_argument("--bvh-width", type=int, default=4, help="rebuilt BVH: 4 (variant 4) or 2 (threaded)")
+    ap.add_argument("--node-format", type=int, default=0, choices=[0, 1],
+                    help="rebuilt 4-wide nodes: 0 = f32 child boxes (128 B), 1 = 8-bit quantised child boxes (64 B)")
     ap.add_argument("--leaf-size", type=int, default=4)
     ap.add_argument("--traversal-cost", type=float, default=2.0)
     ap.add_argument("--no-parity", action="store_true", help="skip the reference-BVH parity frame")
@@ -161,7 +168,8 @@ def cpu_baseline(args, cam_floats, log_fn):
 
 def workload_key(args, spp: int) -> str:
     return (f"{args.scene}_{args.width}x{args.height}_{spp}spp_{args.bounces}b"
-            + ("" if args.bvh == "reference" else f"_rebuilt{args.bvh_width}"))
+            + ("" if args.bvh == "reference" else f"_rebuilt{args.bvh_width}")
+            + ("_q8" if args.node_format else ""))
 
 
 def kernel_source_sha() -> str:
@@ -269,8 +277,10 @@ def main():
     bvh_desc = "reference (bit-exact)"
     if args.bvh == "rebuilt":
         scene = hs.upload(local, bvh="rebuilt", width=args.bvh_width, leaf_size=args.leaf_size,
-                          traversal_cost=args.traversal_cost, gpu_build=not args.host_build)
-        bvh_desc = (f"rebuilt {args.bvh_width}-wide SAH, leaf<={args.leaf_size}, C_trav={args.traversal_cost:g}")
+                          traversal_cost=args.traversal_cost, gpu_build=not args.host_build,
+                          node_format=args.node_format)
+        bvh_desc = (f"rebuilt {args.bvh_width}-wide SAH, leaf<={args.leaf_size}, C_trav={args.traversal_cost:g}"
+                    + (", 8-bit quantised child boxes" if args.node_format else ""))
     t_scene = time.perf_counter() - t
     st = scene.stats()
     counts = hs.counts()
@@ -285,6 +295,10 @@ def main():
     r = crt_amd.Renderer(W, H, local)
     if args.kernel_variant is not None:
         r.set_kernel_variant(args.kernel_variant)
+    if args.regen_threshold is not None:
+        r.set_regen_threshold(args.regen_threshold)
+    if args.critical_tiles is not None:
+        r.set_critical_tiles(args.critical_tiles, args.critical_lanes)
     r.set_camera(cam)
     fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world)
     log_r(f"[plan] {world} rank(s), spp per rank {[fr.spp] if world == 1 else 'spp/N'}")

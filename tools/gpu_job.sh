@@ -9,6 +9,9 @@
 #                                         tools/build_profile_lib.sh), N alternating A B rounds of bench.py ARGS
 #   tools/gpu_job.sh pmc OUT [ARGS..]     rocprofv3 --pmc passes (tools/pmc.sh) over one bench frame
 #   tools/gpu_job.sh l1 OUT               vector-L1 calibration micro-benchmark (tools/probes/l1_probe.hip) + PMC
+#   tools/gpu_job.sh sweep OUT N "label=ARGS" ...
+#                                         N interleaved rounds of bench.py, one run per "label=ARGS" set (the args
+#                                         after '=' split on spaces); one log per label and round
 set -e
 MODE=$1; OUT=gpurun_out/$2; shift 2
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -45,6 +48,16 @@ l1)
   cd /tmp && export TMPDIR=/tmp
   timeout -s KILL 120 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES TCP_PENDING_STALL_CYCLES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE \
       --output-format csv -d $R/$OUT/pmc -o l1 -- $R/tools/probes/l1_probe > $R/$OUT/l1_pmc.log 2>&1
+  ;;
+sweep)
+  N=$1; shift
+  for i in $(seq 1 $N); do
+    for spec in "$@"; do
+      label=${spec%%=*}; args=${spec#*=}
+      timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-count --no-parity $args > $R/$OUT/${label}_$i.log 2>&1
+      echo "$label round $i: $(grep -o '"render_kernel_ms_avg": [0-9.]*' $R/$OUT/${label}_$i.log)"
+    done
+  done
   ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
 esac
