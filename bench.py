@@ -96,8 +96,6 @@ def parse():
     ap.add_argument("--critical-lanes", type=int, default=16, help="their regeneration threshold")
     ap.add_argument("--bvh", default="rebuilt", choices=["rebuilt", "reference"])
     ap.add_argument("--bvh-width", type=int, default=4, help="rebuilt BVH: 4 (variant 4) or 2 (threaded)")
-    ap.add_argument("--node-format", type=int, default=0, choices=[0, 1],
-                    help="rebuilt 4-wide nodes: 0 = f32 child boxes (128 B), 1 = 8-bit quantised child boxes (64 B)")
     ap.add_argument("--leaf-size", type=int, default=4)
     ap.add_argument("--traversal-cost", type=float, default=2.0)
     ap.add_argument("--no-parity", action="store_true", help="skip the reference-BVH parity frame")
@@ -168,8 +166,7 @@ def cpu_baseline(args, cam_floats, log_fn):
 
 def workload_key(args, spp: int) -> str:
     return (f"{args.scene}_{args.width}x{args.height}_{spp}spp_{args.bounces}b"
-            + ("" if args.bvh == "reference" else f"_rebuilt{args.bvh_width}")
-            + ("_q8" if args.node_format else ""))
+            + ("" if args.bvh == "reference" else f"_rebuilt{args.bvh_width}"))
 
 
 def kernel_source_sha() -> str:
@@ -277,10 +274,8 @@ def main():
     bvh_desc = "reference (bit-exact)"
     if args.bvh == "rebuilt":
         scene = hs.upload(local, bvh="rebuilt", width=args.bvh_width, leaf_size=args.leaf_size,
-                          traversal_cost=args.traversal_cost, gpu_build=not args.host_build,
-                          node_format=args.node_format)
-        bvh_desc = (f"rebuilt {args.bvh_width}-wide SAH, leaf<={args.leaf_size}, C_trav={args.traversal_cost:g}"
-                    + (", 8-bit quantised child boxes" if args.node_format else ""))
+                          traversal_cost=args.traversal_cost, gpu_build=not args.host_build)
+        bvh_desc = (f"rebuilt {args.bvh_width}-wide SAH, leaf<={args.leaf_size}, C_trav={args.traversal_cost:g}")
     t_scene = time.perf_counter() - t
     st = scene.stats()
     counts = hs.counts()

@@ -179,9 +179,7 @@ typedef struct crt_scene_options {
     int32_t stack_cap;        /* REBUILT width 4: 0 = the traversal-stack bound computed from the tree (default); > 0
                                  overrides it.  Testing only: a value below the bound makes a render that needs more
                                  entries report CRT_ERR_HIP at synchronisation (the entries are dropped). */
-    int32_t node_format;      /* REBUILT width 4: 0 = f32 child boxes, 128-B nodes (default); 1 = child boxes quantised
-                                 to 8 bits per plane against the node's box, rounded outward, 64-B nodes (one cache
-                                 line; crt_hip.hip wide_boxes_q) */
+    int32_t reserved;
 } crt_scene_options;
 
 /* ---- scene (SceneManager device half) ---- */

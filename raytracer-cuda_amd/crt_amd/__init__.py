@@ -109,16 +109,15 @@ class HostScene:
         return idx, fm
 
     def upload(self, device: int = 0, bvh: str = "reference", leaf_size: int = 0, layouts: int = 0,
-               traversal_cost: float = 0.0, width: int = 0, gpu_build: bool = False, stack_cap: int = 0,
-               node_format: int = 0) -> "Scene":
+               traversal_cost: float = 0.0, width: int = 0, gpu_build: bool = False, stack_cap: int = 0) -> "Scene":
         """Device scene.  bvh="reference": the reference's BVHs, bit-exact (crth_scene_upload);
         bvh="rebuilt": binned-SAH BVH with the reference's hit rule (crt_scene_create_ex)."""
         h = C.c_void_p()
         if (bvh == "reference" and not leaf_size and not layouts and not traversal_cost and not width and not gpu_build
-                and not stack_cap and not node_format):
+                and not stack_cap):
             check_host(_lib.host().crth_scene_upload(self.h, int(device), C.byref(h)), "crth_scene_upload")
             return Scene(h, device)
-        o = scene_options(bvh, leaf_size, layouts, traversal_cost, width, gpu_build, stack_cap, node_format)
+        o = scene_options(bvh, leaf_size, layouts, traversal_cost, width, gpu_build, stack_cap)
         d = self.desc()
         check(_lib.hip().crt_scene_create_ex(C.byref(d), int(device), C.byref(o), C.byref(h)), "crt_scene_create_ex")
         return Scene(h, device)
@@ -142,7 +141,7 @@ class HostScene:
 
 
 def scene_options(bvh: str = "reference", leaf_size: int = 0, layouts: int = 0, traversal_cost: float = 0.0,
-                  width: int = 0, gpu_build: bool = False, stack_cap: int = 0, node_format: int = 0):
+                  width: int = 0, gpu_build: bool = False, stack_cap: int = 0):
     modes = {"reference": _lib.BVH_REFERENCE, "rebuilt": _lib.BVH_REBUILT}
     if bvh not in modes:
         raise ValueError(f"bvh must be one of {sorted(modes)}")
@@ -152,7 +151,6 @@ def scene_options(bvh: str = "reference", leaf_size: int = 0, layouts: int = 0, 
     o.width = int(width)
     o.gpu_build = int(bool(gpu_build))
     o.stack_cap = int(stack_cap)
-    o.node_format = int(node_format)
     return o
 
 

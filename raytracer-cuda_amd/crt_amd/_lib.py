@@ -77,7 +77,7 @@ class SceneStats(C.Structure):
 class SceneOptions(C.Structure):
     _fields_ = [("bvh", C.c_int32), ("leaf_size", C.c_int32), ("layouts", C.c_int32),
                 ("traversal_cost", C.c_float), ("width", C.c_int32), ("gpu_build", C.c_int32),
-                ("stack_cap", C.c_int32), ("node_format", C.c_int32)]
+                ("stack_cap", C.c_int32), ("reserved", C.c_int32)]
 
 
 BVH_REFERENCE = 0

@@ -603,66 +603,6 @@ __device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ nodes, ui
     return w;
 }
 
-// Quantised 4-wide node (crt_scene_options.node_format 1): 64 B, one cache line, 4 rows where the f32 node has 7.
-//   row 0: origin.xyz, first_child          row 1: scale.xyz (powers of two), n_int | n_slots << 8
-//   row 2: qlo.x, qhi.x, qlo.y, qhi.y       row 3: qlo.z, qhi.z, leaf_first, counts
-// Each q word holds one byte per slot: the child's plane is origin + q * scale, rounded outward from the padded f32
-// box on the host (quantize_nodes4), so every quantised box contains the f32 one and the closest-hit rule is
-// unchanged (a box can only gain hits).  Empty slots hold qlo 255 / qhi 0, an inverted box that is never hit.
-// t = q * (scale * inv) + (origin * inv - o * inv): scale * inv is exact (a power of two), and the error of the
-// two roundings of the sum is of the order of the f32 form's, far inside the boxes' padding.  The entry and exit
-// rows are chosen per axis by the sign of 1/d, as in wide_boxes.  Row k of node n sits at slot k ^ (n & 3).
-__device__ __forceinline__ uint32_t qnode_base(int node) { return ((uint32_t)node << 6) | (((uint32_t)node & 3u) << 4); }
-__device__ __forceinline__ Wide4 wide_boxes_q(const float4* __restrict__ nodes, uint32_t b, V3 o, V3 inv, float tmax,
-                                              float4& r0, float4& r1, float4& r3) {
-    r0 = *rec_at(nodes, b);
-    r1 = *rec_at(nodes, b ^ 16u);
-    const float4 r2 = *rec_at(nodes, b ^ 32u);
-    r3 = *rec_at(nodes, b ^ 48u);
-    const float nx = -(o.x * inv.x), ny = -(o.y * inv.y), nz = -(o.z * inv.z);
-    const float bx = __builtin_fmaf(r0.x, inv.x, nx), by = __builtin_fmaf(r0.y, inv.y, ny), bz = __builtin_fmaf(r0.z, inv.z, nz);
-    const float sx = r1.x * inv.x, sy = r1.y * inv.y, sz = r1.z * inv.z;
-    const bool px = (int)__float_as_uint(inv.x) >= 0, py = (int)__float_as_uint(inv.y) >= 0,
-               pz = (int)__float_as_uint(inv.z) >= 0;
-    const uint32_t lx = __float_as_uint(r2.x), hx = __float_as_uint(r2.y), ly = __float_as_uint(r2.z),
-                   hy = __float_as_uint(r2.w), lz = __float_as_uint(r3.x), hz = __float_as_uint(r3.y);
-    const uint32_t ex = px ? lx : hx, fx = px ? hx : lx, ey = py ? ly : hy, fy = py ? hy : ly;
-    const uint32_t ez = pz ? lz : hz, fz = pz ? hz : lz;
-    auto pair = [](uint32_t q, int s, float sc, float bs) -> pf2 {
-        const pf2 v = {(float)((q >> (8 * s)) & 0xffu), (float)((q >> (8 * s + 8)) & 0xffu)};
-        return __builtin_elementwise_fma(v, (pf2){sc, sc}, (pf2){bs, bs});
-    };
-    const pf2 ax0 = pair(ex, 0, sx, bx), ax1 = pair(ex, 2, sx, bx), bx0 = pair(fx, 0, sx, bx), bx1 = pair(fx, 2, sx, bx);
-    const pf2 ay0 = pair(ey, 0, sy, by), ay1 = pair(ey, 2, sy, by), by0 = pair(fy, 0, sy, by), by1 = pair(fy, 2, sy, by);
-    const pf2 az0 = pair(ez, 0, sz, bz), az1 = pair(ez, 2, sz, bz), bz0 = pair(fz, 0, sz, bz), bz1 = pair(fz, 2, sz, bz);
-    const float ax[4] = {ax0.x, ax0.y, ax1.x, ax1.y}, bxs[4] = {bx0.x, bx0.y, bx1.x, bx1.y};
-    const float ay[4] = {ay0.x, ay0.y, ay1.x, ay1.y}, bys[4] = {by0.x, by0.y, by1.x, by1.y};
-    const float az[4] = {az0.x, az0.y, az1.x, az1.y}, bzs[4] = {bz0.x, bz0.y, bz1.x, bz1.y};
-    Wide4 w;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const float t0 = fmaxf(fmaxf(ax[s], ay[s]), fmaxf(az[s], 0.001f));
-        const float t1 = fminf(fminf(bxs[s], bys[s]), fminf(bzs[s], tmax));
-        w.tmin[s] = t0;
-        w.hit[s] = t0 < t1;
-    }
-    return w;
-}
-// The link row of either node format: (first_child, n_int | n_slots << 8, leaf_first, counts).
-template <bool QN>
-__device__ __forceinline__ Wide4 node_boxes(const float4* __restrict__ nodes, int node, V3 o, V3 inv, float tmax,
-                                            float4& link) {
-    if (QN) {
-        float4 r0, r1, r3;
-        const Wide4 w = wide_boxes_q(nodes, qnode_base(node), o, inv, tmax, r0, r1, r3);
-        link = make_float4(r0.w, r1.w, r3.z, r3.w);
-        return w;
-    }
-    const uint32_t b = node_base(node);
-    link = node_row(nodes, b, 6);
-    return wide_boxes(nodes, b, o, inv, tmax);
-}
-
 // Spheres kept out of a 4-wide BVH (scenes with few spheres) are tested once per ray, before the traversal;
 // the hit rule is order-independent, so this is the same closest hit.  A sphere is reached only if the
 // reference's scene-level boxes on its path pass AABB::hit against [0.001, inf) with the exact 1/d: the
@@ -771,16 +711,16 @@ __device__ __forceinline__ void cas(uint32_t& a, uint32_t& b) {
 // Per-lane closest hit over a 4-wide BVH (diagnostic path: crt_scene_compare).  Returns the rank or -1.
 __device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict__ prims,
                       const float4* __restrict__ chain, int n_chain, int sphere_first, int n_spheres, V3 o, V3 d,
-                      float& closest, int qn) {
+                      float& closest) {
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     closest = __builtin_inff();
     int hit = -1, node = 0, sp = 0;
     ray_spheres(prims, chain, n_chain, sphere_first, n_spheres, o, d, inv, closest, hit);
     int stack[64];
     while (node >= 0) {
-        float4 mf;
-        const Wide4 w = qn ? node_boxes<true>(nodes, node, o, box_inv(inv), closest, mf)
-                           : node_boxes<false>(nodes, node, o, box_inv(inv), closest, mf);
+        const uint32_t b = node_base(node);
+        const Wide4 w = wide_boxes(nodes, b, o, box_inv(inv), closest);
+        const float4 mf = node_row(nodes, b, 6);
         const int first_child = __float_as_int(mf.x), n_int = __float_as_int(mf.y) & 0xff;
         const uint32_t counts = __float_as_uint(mf.w);
         int off = 0;
@@ -833,24 +773,16 @@ __device__ __forceinline__ int lane_fresh() {
     return l;
 }
 
-template <bool COUNT, bool QN>
+template <bool COUNT>
 __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, int& node, int& sp, float closest,
                                            TraceCounts& cnt, uint32_t* __restrict__ stk, int lane, size_t pix,
                                            size_t n_pix, int& leaf_first, int& leaf_n) {
     leaf_n = 0;
     leaf_first = 0;
     if (node >= 0) {
-        float4 mf;
-        Wide4 w;
-        if constexpr (QN) {
-            float4 r0, r1, r3;
-            w = wide_boxes_q(P.nodes, qnode_base(node), o, inv, closest, r0, r1, r3);
-            mf = make_float4(r0.w, r1.w, r3.z, r3.w);
-        } else {
-            const uint32_t b = node_base(node);
-            mf = node_row(P.nodes, b, 6);
-            w = wide_boxes(P.nodes, b, o, inv, closest);
-        }
+        const uint32_t b = node_base(node);
+        const float4 mf = node_row(P.nodes, b, 6);
+        const Wide4 w = wide_boxes(P.nodes, b, o, inv, closest);
         // keep the whole link row in the node's loads: left to itself the compiler loads leaf_first / counts
         // only inside the leaf branch, one more dependent load on a leaf step's critical path.  Pinned after the
         // box tests, so the wait it implies is the one the boxes need anyway (pinned before them, it made the six
@@ -910,14 +842,14 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
     }
 }
 
-template <bool COUNT, bool QN>
+template <bool COUNT>
 __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d, V3 inv, int& node, int& sp,
                                                float& closest, int& hit, TraceCounts& cnt, WaveLds& L,
                                                uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix) {
     if (COUNT) cnt.step_slots++;
     const uint64_t c0 = COUNT ? shader_clock() : 0;
     int leaf_n, leaf_first;
-    node_step4<COUNT, QN>(P, o, inv, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
+    node_step4<COUNT>(P, o, inv, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
     const uint64_t c1 = COUNT ? shader_clock() : 0;
     if (COUNT) cnt.cyc_step += c1 - c0;
     if (!__ballot(leaf_n > 0)) return;
@@ -1112,13 +1044,10 @@ __device__ unsigned long long g_wave_prof[2 * 4 * 65536];
 
 // Waves per workgroup: 4 (16x16 pixels), or 1 for variant 8 (one 8x8 tile per workgroup, so a finished wave frees
 // its slot at once instead of holding it until its three siblings end).
-template <int VARIANT> struct KernelShape { static constexpr int waves = VARIANT % 10 == 8 ? 1 : 4; };
+template <int VARIANT> struct KernelShape { static constexpr int waves = VARIANT == 8 ? 1 : 4; };
 
-// VARIANT + 10: the same variant over quantised 4-wide nodes (crt_scene_options.node_format 1, wide_boxes_q).
-template <bool COUNT, int VARIANT_, int MINW>
-__global__ __launch_bounds__(64 * KernelShape<VARIANT_>::waves, MINW) void crt_render_kernel(RenderParams P) {
-    constexpr int VARIANT = VARIANT_ % 10;
-    constexpr bool QN = VARIANT_ >= 10;
+template <bool COUNT, int VARIANT, int MINW>
+__global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_render_kernel(RenderParams P) {
 #ifdef CRT_PROFILE_WAVE_TIMES
     const unsigned long long prof_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1280,7 +1209,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT_>::waves, MINW) void crt_r
                 if (!__ballot(live)) break;      // the queue is empty and every lane is done
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
-            traverse_step4<COUNT, QN>(P, S.o, S.d, inv, node, sp, closest, hit, cnt, L, stk, lane, (size_t)ppix, n_pix);
+            traverse_step4<COUNT>(P, S.o, S.d, inv, node, sp, closest, hit, cnt, L, stk, lane, (size_t)ppix, n_pix);
         }
     } else if (WIDE) {
         // Same scheduling as variant 3 over a 4-wide BVH: node < 0 = no node left (lane parked).
@@ -1340,7 +1269,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT_>::waves, MINW) void crt_r
                 if (TILED) wave_rays += (uint32_t)__popcll(__ballot(parked && has_result));
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
-            traverse_step4<COUNT, QN>(P, S.o, S.d, inv, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
+            traverse_step4<COUNT>(P, S.o, S.d, inv, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
         }
     } else if (VARIANT == 2 || VARIANT == 3) {
         constexpr bool PF = VARIANT == 3;
@@ -1453,7 +1382,6 @@ struct CompareParams {
     const float4* __restrict__ prims_b;
     int n_nodes_b, n_layouts_b;
     int width_a, width_b;
-    int qn_a, qn_b;       // width 4: quantised node format (wide_boxes_q)
     int sphere_first_b, n_spheres_b;
     const float4* chain_b;
     int n_chain_b;
@@ -1492,11 +1420,11 @@ __global__ __launch_bounds__(256) void crt_compare_kernel(CompareParams Q) {
         ++S.rays;
         float ta, tb;
         const int ha = Q.width_a == 4 ? trace4(P.nodes, P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres,
-                                               S.o, S.d, ta, Q.qn_a)
+                                               S.o, S.d, ta)
                                       : trace<false>(P.nodes, P.prims, P.n_nodes, layout_base(S.d, P.n_layouts, P.n_nodes),
                                                      S.o, S.d, ta, cnt);
         const int hb = Q.width_b == 4 ? trace4(Q.nodes_b, Q.prims_b, Q.chain_b, Q.n_chain_b, Q.sphere_first_b, Q.n_spheres_b,
-                                               S.o, S.d, tb, Q.qn_b)
+                                               S.o, S.d, tb)
                                       : trace<false>(Q.nodes_b, Q.prims_b, Q.n_nodes_b,
                                                      layout_base(S.d, Q.n_layouts_b, Q.n_nodes_b), S.o, S.d, tb, cnt);
         if (ha != hb) {
@@ -2199,7 +2127,6 @@ struct crt_scene {
     int sphere_first = 0, n_ray_spheres = 0;   // width 4: spheres tested per ray, prims [first, first + n)
     float sph2[2][12] = {};                    // width 4 with exactly two per-ray spheres: their kernel-argument copy
     int tree_spheres = 1;                      // width 4: some leaf holds a sphere
-    int node_format = 0;                       // width 4: 1 = quantised 64-B nodes (wide_boxes_q)
     long excluded = 0;
 };
 
@@ -2291,8 +2218,6 @@ static int build_scene_arrays(const crt_scene_desc* D, const crt_scene_options* 
     if (!(o.traversal_cost > 0.f && o.traversal_cost <= 64.f)) return set_error(CRT_ERR_INVALID_ARGUMENT, "traversal_cost must be in (0, 64]");
     if (o.leaf_size < 1 || o.leaf_size > 16) return set_error(CRT_ERR_INVALID_ARGUMENT, "leaf_size must be 1..16");
     if (o.layouts != 1 && o.layouts != 6) return set_error(CRT_ERR_INVALID_ARGUMENT, "layouts must be 1 or 6");
-    if (o.node_format != 0 && !(o.node_format == 1 && o.bvh == CRT_BVH_REBUILT && o.width == 4))
-        return set_error(CRT_ERR_INVALID_ARGUMENT, "node_format 1 needs the rebuilt 4-wide BVH");
     if (D->n_scene_nodes <= 0 || !D->scene_nodes) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene has no BVH nodes");
     if (D->n_materials < 0 || (D->n_materials > 0 && !D->materials)) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad materials");
     if (!F.build_triangles() || !F.emit_scene(0, 0, false)) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene: " + F.err);
@@ -2307,54 +2232,6 @@ static int build_scene_arrays(const crt_scene_desc* D, const crt_scene_options* 
     return CRT_OK;
 }
 
-// The rebuilt tree's 4-wide nodes (8 float4 rows each, emit4) as quantised 64-B nodes (4 float4 rows; format at
-// wide_boxes_q).  Per node and axis: origin = the lowest child plane, scale = the smallest power of two with
-// origin + 255 * scale >= the highest child plane; a child's lo plane rounds down and its hi plane up to the grid, so
-// each quantised box contains the (already padded) f32 box.  Empty slots get lo 255 / hi 0: an inverted box, never
-// hit.  Rows are not swizzled here (crt_scene_create_ex does it).
-static std::vector<float4> quantize_nodes4(const std::vector<float4>& nodes) {
-    const size_t n_nodes = nodes.size() / 8;
-    std::vector<float4> out(4 * n_nodes);
-    for (size_t n = 0; n < n_nodes; ++n) {
-        const float4* R = &nodes[8 * n];
-        const float4 meta = R[6];
-        const int n_slots = (i2i_host(meta.y) >> 8) & 0xff;
-        float origin[3] = {0.f, 0.f, 0.f}, scale[3] = {1.f, 1.f, 1.f};
-        uint32_t qlo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, qhi[3] = {0u, 0u, 0u};
-        for (int a = 0; a < 3; ++a) {
-            const float* lo = &R[2 * a].x;
-            const float* hi = &R[2 * a + 1].x;
-            if (n_slots == 0) continue;
-            float mn = lo[0], mx = hi[0];
-            for (int s = 1; s < n_slots; ++s) { mn = std::min(mn, lo[s]); mx = std::max(mx, hi[s]); }
-            const double ext = (double)mx - (double)mn;
-            int e = -126;
-            if (ext > 0) e = std::max(-126, (int)std::ceil(std::log2(ext / 255.0)));
-            while ((double)mn + 255.0 * std::ldexp(1.0, e) < (double)mx) ++e;
-            const double sc = std::ldexp(1.0, e);
-            origin[a] = mn;
-            scale[a] = (float)sc;
-            for (int s = 0; s < n_slots; ++s) {
-                double ql = std::floor(((double)lo[s] - (double)mn) / sc);
-                double qh = std::ceil(((double)hi[s] - (double)mn) / sc);
-                ql = std::min(255.0, std::max(0.0, ql));
-                qh = std::min(255.0, std::max(0.0, qh));
-                while (ql > 0 && (double)mn + ql * sc > (double)lo[s]) ql -= 1;
-                while (qh < 255 && (double)mn + qh * sc < (double)hi[s]) qh += 1;
-                const uint32_t m = 0xffu << (8 * s);
-                qlo[a] = (qlo[a] & ~m) | ((uint32_t)ql << (8 * s));
-                qhi[a] = (qhi[a] & ~m) | ((uint32_t)qh << (8 * s));
-            }
-        }
-        auto u = [](uint32_t v) { float f; std::memcpy(&f, &v, 4); return f; };
-        out[4 * n + 0] = make_float4(origin[0], origin[1], origin[2], meta.x);                 // first_child
-        out[4 * n + 1] = make_float4(scale[0], scale[1], scale[2], meta.y);                    // n_int | n_slots << 8
-        out[4 * n + 2] = make_float4(u(qlo[0]), u(qhi[0]), u(qlo[1]), u(qhi[1]));
-        out[4 * n + 3] = make_float4(u(qlo[2]), u(qhi[2]), meta.z, meta.w);                    // leaf_first, counts
-    }
-    return out;
-}
-
 extern "C" {
 
 int crt_scene_export(const crt_scene_desc* D, const crt_scene_options* opts, float* nodes, float* prims,
@@ -2365,8 +2242,7 @@ int crt_scene_export(const crt_scene_desc* D, const crt_scene_options* opts, flo
     Rebuilt RB;
     if (int rc = build_scene_arrays(D, opts, o, F, RB, 0)) return rc;
     const bool rebuilt = o.bvh == CRT_BVH_REBUILT;
-    const std::vector<float4> Q = o.node_format == 1 ? quantize_nodes4(RB.nodes) : std::vector<float4>();
-    const std::vector<float4>& N = o.node_format == 1 ? Q : rebuilt ? RB.nodes : F.nodes;
+    const std::vector<float4>& N = rebuilt ? RB.nodes : F.nodes;
     const std::vector<float4>& Pr = rebuilt ? RB.prims : F.prims;
     const std::vector<int>& rc = rebuilt ? RB.rank_code : F.rank_code;
     info[0] = (int64_t)N.size();
@@ -2487,16 +2363,8 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
         return e;
     };
     const std::vector<int>& rc = rebuilt ? RB.rank_code : F.rank_code;
-    // width 4: row k of node n at slot k ^ (n & 7) of its 128-B record (node_row), or k ^ (n & 3) of its 64-B
-    // quantised record (wide_boxes_q)
-    std::vector<float4> swizzled;
-    S->node_format = rebuilt && S->width == 4 ? o.node_format : 0;
-    if (S->width == 4 && S->node_format == 1) {
-        const std::vector<float4> q = quantize_nodes4(RB.nodes);
-        swizzled.resize(q.size());
-        for (size_t n = 0; n < q.size() / 4; ++n)
-            for (size_t k = 0; k < 4; ++k) swizzled[4 * n + (k ^ (n & 3))] = q[4 * n + k];
-    } else if (S->width == 4) {
+    std::vector<float4> swizzled;   // width 4: row k of node n at slot k ^ (n & 7) of its record (node_row)
+    if (S->width == 4) {
         swizzled.resize(RB.nodes.size());
         for (size_t n = 0; n < RB.nodes.size() / 8; ++n)
             for (size_t k = 0; k < 8; ++k) swizzled[8 * n + (k ^ (n & 7))] = RB.nodes[8 * n + k];
@@ -2520,7 +2388,7 @@ int crt_scene_get_stats(const crt_scene* S, crt_scene_stats* out) {
     out->width = S->width;
     out->stack_bound = S->stack_cap;
     out->device_prims = S->n_prims;
-    out->device_bytes = (int64_t)S->n_nodes * S->layouts * (S->width == 4 ? (S->node_format == 1 ? 64 : 128) : 32) + (int64_t)S->n_prims * 48 + (int64_t)S->n_mats * 48 +
+    out->device_bytes = (int64_t)S->n_nodes * S->layouts * (S->width == 4 ? 128 : 32) + (int64_t)S->n_prims * 48 + (int64_t)S->n_mats * 48 +
                         (int64_t)S->n_ranks * 48;
     out->max_depth = S->max_depth;
     out->n_materials = S->n_mats;
@@ -2716,8 +2584,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.n_chain = S->n_chain;
     P.tree_spheres = S->tree_spheres;
     std::memcpy(P.sph2, S->sph2, sizeof P.sph2);
-    // quantised 4-wide nodes are instantiated at occupancy 6 only
-    const int occ = S->node_format ? 6 : R->min_waves ? R->min_waves : (S->width == 4 ? 6 : 5);
+    const int occ = R->min_waves ? R->min_waves : (S->width == 4 ? 6 : 5);
     P.stack_lds = std::min(R->stack_lds, occ >= 7 ? 11 : occ >= 6 ? 12 : STACK_LDS);
     if (S->width == 4 && S->stack_cap > P.stack_lds) {
         const size_t need = (size_t)(S->stack_cap - P.stack_lds);
@@ -2771,8 +2638,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             Q.spp = probe_spp_for(R, spp);
             Q.accumulate = 0;
             Q.probe_cost = R->d_tile_cost;
-            if (S->node_format) hipLaunchKernelGGL((crt_render_kernel<true, 14, 6>), grid, block, 0, st, Q);
-            else if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<true, 4, 6>), grid, block, 0, st, Q);
+            if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<true, 4, 6>), grid, block, 0, st, Q);
             else hipLaunchKernelGGL((crt_render_kernel<true, 4, 5>), grid, block, 0, st, Q);
             hipLaunchKernelGGL(crt_tile_cost_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_tile_cost,
                                R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode);
@@ -2793,11 +2659,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         }
         const dim3 tgrid(n_tiles), tblock(64);
         const char* cs = cnt ? "true" : "false";
-        if (S->node_format) {       // quantised nodes: occupancy 6 only
-            std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 18, 6>", cs);
-            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 18, 6>), tgrid, tblock, 0, st, P);
-            else hipLaunchKernelGGL((crt_render_kernel<false, 18, 6>), tgrid, tblock, 0, st, P);
-        } else if (occ >= 7) {
+        if (occ >= 7) {
             std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 8, 7>", cs);
             if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 8, 7>), tgrid, tblock, 0, st, P);
             else hipLaunchKernelGGL((crt_render_kernel<false, 8, 7>), tgrid, tblock, 0, st, P);
@@ -2829,8 +2691,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             Q.spp = probe_spp_for(R, spp);
             Q.accumulate = 0;
             Q.probe_cost = R->d_tile_cost;
-            if (S->node_format) hipLaunchKernelGGL((crt_render_kernel<false, 14, 6>), grid, block, 0, st, Q);
-            else if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<false, 4, 6>), grid, block, 0, st, Q);
+            if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<false, 4, 6>), grid, block, 0, st, Q);
             else hipLaunchKernelGGL((crt_render_kernel<false, 4, 5>), grid, block, 0, st, Q);
             const unsigned ob = (unsigned)((n_pix + ORDER_ITEMS - 1) / ORDER_ITEMS);
             HIP_TRY(hipMemsetAsync(R->d_order_hist, 0, ORDER_KEYS * 4, st));
@@ -2851,11 +2712,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         const int per_cu = occ >= 7 ? 7 : occ >= 6 ? 6 : 5;        // workgroups of 4 waves resident per CU
         const int n_wg = std::max(1, std::min(R->n_cus * per_cu, (int)((n_pix + 255) / 256)));
         const dim3 pgrid(n_wg);
-        if (S->node_format) {
-            std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 17, 6>", cnt ? "true" : "false");
-            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 17, 6>), pgrid, block, 0, st, P);
-            else hipLaunchKernelGGL((crt_render_kernel<false, 17, 6>), pgrid, block, 0, st, P);
-        } else if (occ >= 7) {
+        if (occ >= 7) {
             std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 7, 7>", cnt ? "true" : "false");
             if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 7, 7>), pgrid, block, 0, st, P);
             else hipLaunchKernelGGL((crt_render_kernel<false, 7, 7>), pgrid, block, 0, st, P);
@@ -2869,8 +2726,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             else hipLaunchKernelGGL((crt_render_kernel<false, 7, 5>), pgrid, block, 0, st, P);
         }
     } else if (S->width == 4) {
-        if (S->node_format) CRT_LAUNCH(14, 6);
-        else if (occ >= 7) CRT_LAUNCH(4, 7);
+        if (occ >= 7) CRT_LAUNCH(4, 7);
         else if (occ >= 6) CRT_LAUNCH(4, 6);
         else if (occ >= 5) CRT_LAUNCH(4, 5);
         else if (occ >= 4) CRT_LAUNCH(4, 4);
@@ -2921,7 +2777,6 @@ int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene*
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     Q.nodes_b = B->d_nodes; Q.prims_b = B->d_prims; Q.n_nodes_b = B->n_nodes; Q.n_layouts_b = B->layouts;
     Q.width_a = A->width; Q.width_b = B->width;
-    Q.qn_a = A->node_format; Q.qn_b = B->node_format;
     Q.dump = nullptr;
     Q.max_dump = 0;
     float* d_dump = nullptr;

@@ -16,8 +16,7 @@ pytestmark = pytest.mark.gpu
 RMS_TOL = 1e-4
 
 CONFIGS = {"w4": dict(width=4), "w4l8": dict(width=4, leaf_size=8, traversal_cost=2),
-           "w2l16": dict(width=2, leaf_size=16, traversal_cost=6),
-           "w4q": dict(width=4, node_format=1)}     # child boxes quantised to 8 bits, 64-B nodes (wide_boxes_q)
+           "w2l16": dict(width=2, leaf_size=16, traversal_cost=6)}
 
 
 @pytest.fixture(scope="module")
@@ -225,44 +224,3 @@ def _schedule_case(rebuilt, variant, probe_spp, crit=None, **flags):
     b.synchronize()
     assert np.array_equal(a.linear().view(np.uint32), b.linear().view(np.uint32))
     assert np.array_equal(a.rng_state(), b.rng_state())
-
-
-@pytest.mark.parametrize("variant", [7, 8])
-@pytest.mark.parametrize("w,h,spp", [(160, 90, 8), (100, 37, 70), (9, 1, 65)])
-def test_quantized_variants_are_bit_identical(rebuilt, w, h, spp, variant):
-    """Quantised 4-wide nodes: variants 7 and 8 (kernel instantiations 17 and 18) give variant 4's (14's) frame,
-    RNG state and ray count, with the overflow stack and the probe order exercised."""
-    dev = rebuilt["cornell_bunny", "w4q"]
-    cam = crt_amd.camera(spp)
-    a = _frame(dev, w, h, spp, 20, cam, variant=4)
-    b = _frame(dev, w, h, spp, 20, cam, variant=variant)
-    c = _frame(dev, w, h, spp, 20, cam, variant=4, stack_lds=1)
-    for r in (b, c):
-        assert np.array_equal(a.linear().view(np.uint32), r.linear().view(np.uint32))
-        assert np.array_equal(a.rng_state(), r.rng_state())
-        assert a.counters()["rays"] == r.counters()["rays"]
-    assert a.last_kernel_name() == "crt_render_kernel<false, 14, 6>"
-    assert b.last_kernel_name() == f"crt_render_kernel<false, {10 + variant}, 6>"
-
-
-def test_quantized_counting_kernel(rebuilt):
-    """The counting kernel on quantised nodes: same rays and frame as the timed kernel, and box tests at least the
-    f32 tree's minus a small margin (a quantised box contains the f32 box, so it is entered at least as often; the
-    paths themselves may fork where a rounding differs)."""
-    cam = crt_amd.camera(4)
-    out = {}
-    for cfg in ("w4", "w4q"):
-        r = crt_amd.Renderer(96, 54)
-        r.set_kernel_variant(8)
-        r.set_camera(cam)
-        r.init_rand(41)
-        r.render(rebuilt["cornell_bunny", cfg], 4, 20, count_work=True)
-        r.synchronize()
-        out[cfg] = r.counters()
-        lin = r.linear()
-        r.init_rand(41)
-        r.render(rebuilt["cornell_bunny", cfg], 4, 20)
-        r.synchronize()
-        assert np.array_equal(lin.view(np.uint32), r.linear().view(np.uint32))
-        assert r.counters()["rays"] == out[cfg]["rays"]
-    assert out["w4q"]["box_tests"] >= 0.99 * out["w4"]["box_tests"] * out["w4q"]["rays"] / out["w4"]["rays"]

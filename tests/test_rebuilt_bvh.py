@@ -324,117 +324,3 @@ def test_ground_sphere_box_culls_spurious_root():
         tmin = max(max(min(t0[0], t1[0]), min(t0[1], t1[1])), min(t0[2], t1[2]), F32(0.001))
         tmax = min(max(t0[0], t1[0]), max(t0[1], t1[1]), max(t0[2], t1[2]))
         assert tmax <= tmin, "the reference's sphere box test rejects the ray"
-
-
-# ---------------------------------------------------------------- quantised 4-wide nodes (node_format 1)
-def _dequantize(eq):
-    """Quantised export (4 rows per node, crt_hip.hip wide_boxes_q) -> per node/slot/axis float64 planes + link row."""
-    q = eq["nodes"].reshape(-1, 4, 4)
-    origin, scale = q[:, 0, :3].astype(np.float64), q[:, 1, :3].astype(np.float64)
-    words = q[:, 2:4, :].reshape(-1, 8).view(np.uint32)        # qlo.x qhi.x qlo.y qhi.y qlo.z qhi.z leaf_first counts
-    by = ((words[:, :6, None] >> (8 * np.arange(4, dtype=np.uint32))) & 0xFF).astype(np.float64)   # [n, 6, slot]
-    lo = origin[:, :, None] + by[:, 0::2, :] * scale[:, :, None]      # [n, axis, slot]
-    hi = origin[:, :, None] + by[:, 1::2, :] * scale[:, :, None]
-    link = np.stack([q[:, 0, 3], q[:, 1, 3], q[:, 3, 2], q[:, 3, 3]], 1)
-    return lo, hi, by, scale, link
-
-
-def test_quantized_nodes_contain_float_boxes(host_scene):
-    e = host_scene.export("rebuilt", width=4)
-    eq = host_scene.export("rebuilt", width=4, node_format=1)
-    assert eq["node_float4s"] == e["node_float4s"] // 2
-    for k in ("prim_float4s", "ranks", "stack_bound", "sphere_first", "n_ray_spheres"):
-        assert eq[k] == e[k]
-    nf = e["nodes"].reshape(-1, 8, 4)
-    lo, hi, by, scale, link = _dequantize(eq)
-    assert np.array_equal(link.view(np.int32), nf[:, 6].view(np.int32)), "link row preserved"
-    m, e2 = np.frexp(scale)
-    assert (m == 0.5).all(), "scales are powers of two"
-    n_slots = nf[:, 6].view(np.int32)[:, 1] >> 8
-    flo = nf[:, 0:6:2, :].astype(np.float64)      # [n, axis, slot]
-    fhi = nf[:, 1:6:2, :].astype(np.float64)
-    live = np.arange(4)[None, None, :] < n_slots[:, None, None]
-    live = np.broadcast_to(live, flo.shape)
-    assert (lo[live] <= flo[live]).all() and (hi[live] >= fhi[live]).all(), "quantised box must contain the f32 box"
-    step = np.broadcast_to(scale[:, :, None], flo.shape)
-    assert (flo[live] - lo[live] < step[live]).all() and (hi[live] - fhi[live] < step[live]).all(), "one step at most"
-    dead = ~live
-    assert (by[:, 0::2, :][dead] == 255).all() and (by[:, 1::2, :][dead] == 0).all(), "empty slots inverted"
-    # the scale is the smallest power of two whose 255 steps span the node's extent on that axis
-    ext = fhi.max(2, where=live, initial=-np.inf) - flo.min(2, where=live, initial=np.inf)
-    ok = np.isfinite(ext) & (ext > 0)
-    assert (255 * scale[ok] >= ext[ok]).all() and (127.5 * scale[ok] < ext[ok]).all()
-
-
-def _trace_wide_q(eq, prims, ranks, o, d):
-    """_trace_wide over the quantised nodes, planes evaluated as the kernel does: q * (scale * inv) + (origin * inv
-    - o * inv) in float32 with a single rounding for the fused steps (emulated in float64, then rounded)."""
-    lo, hi, by, scale, link = _dequantize(eq)
-    q = eq["nodes"].reshape(-1, 4, 4)
-    with np.errstate(all="ignore"):
-        inv = (F32(1) / d).astype(np.float32)
-    inv = np.clip(inv, -F32(2.0 ** 64), F32(2.0 ** 64)).astype(np.float32)
-    noi = (-(o * inv)).astype(np.float32)
-    closest, hit = np.float32(np.inf), -1
-    rs = slice(eq["sphere_first"], eq["sphere_first"] + eq["n_ray_spheres"])
-    if eq["n_ray_spheres"]:
-        closest, hit = _best(_prim_t(prims[rs], o, d, np.float32(np.inf)), ranks[rs])
-    stack, node = [], 0
-    while node >= 0:
-        org, sc = q[node, 0, :3], q[node, 1, :3]
-        base = np.float32(org.astype(np.float64) * inv + noi)                    # fma(origin, inv, -o*inv)
-        sinv = (sc * inv).astype(np.float32)
-        a = [np.float32(by[node, 2 * k] * np.float64(sinv[k]) + np.float64(base[k])) for k in range(3)]
-        b = [np.float32(by[node, 2 * k + 1] * np.float64(sinv[k]) + np.float64(base[k])) for k in range(3)]
-        ent = [np.where(inv[k] >= 0, a[k], b[k]) for k in range(3)]
-        ext = [np.where(inv[k] >= 0, b[k], a[k]) for k in range(3)]
-        t0 = np.fmax(np.fmax(ent[0], ent[1]), np.fmax(ent[2], F32(0.001)))
-        t1 = np.fmin(np.fmin(ext[0], ext[1]), np.fmin(ext[2], closest))
-        hitm = t0 < t1
-        fc, meta, lf, counts = _i(link[node])
-        n_int = meta & 0xFF
-        entry = closest
-        off = 0
-        for s in range(4):
-            c = (counts >> (8 * s)) & 0xFF
-            if s >= n_int and c and hitm[s]:
-                rng = slice(lf + off, lf + off + c)
-                closest, hit = _best(_prim_t(prims[rng], o, d, entry), ranks[rng], closest, hit)
-            off += c
-        kids = sorted((t0[s], s) for s in range(n_int) if hitm[s])
-        if kids:
-            node = fc + kids[0][1]
-            stack.extend(fc + s for _, s in reversed(kids[1:]))
-        else:
-            node = stack.pop() if stack else -1
-    return closest, hit
-
-
-def test_quantized_traversal_equals_brute_force(host_scene):
-    eq = host_scene.export("rebuilt", width=4, node_format=1)
-    prims = eq["prims"].reshape(-1, 3, 4)
-    ranks = _prim_ranks(eq["prims"])
-    rng = np.random.default_rng(11)
-    n_hit = 0
-    for i in range(120):
-        if i % 2:
-            o = rng.uniform([-0.25, 0.0, -0.25], [0.25, 0.5, 0.25]).astype(np.float32)
-            tgt = np.array([-0.096, 0.14, -0.078], np.float32) + rng.normal(0, 0.04, 3).astype(np.float32)
-            d = (tgt - o).astype(np.float32)
-        else:
-            o = rng.uniform([-0.27, 0.01, -0.27], [0.27, 0.54, 0.3]).astype(np.float32)
-            d = rng.normal(size=3).astype(np.float32)
-        brute = _best(_prim_t(prims, o, d, np.float32(np.inf)), ranks)
-        got = _trace_wide_q(eq, prims, ranks, o, d)
-        assert got[1] == brute[1] and got[0].view(np.uint32) == np.float32(brute[0]).view(np.uint32), (i, got, brute)
-        n_hit += got[1] >= 0
-    assert n_hit > 80
-
-
-def test_quantized_export_errors(host_scene):
-    with pytest.raises(RuntimeError):
-        host_scene.export("rebuilt", width=2, node_format=1)
-    with pytest.raises(RuntimeError):
-        host_scene.export("reference", node_format=1)
-    with pytest.raises(RuntimeError):
-        host_scene.export("rebuilt", width=4, node_format=2)
