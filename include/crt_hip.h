@@ -271,6 +271,8 @@ int  crt_renderer_get_schedule_stats(crt_renderer* r, unsigned long long* out3);
  * {shading/regeneration passes, traversal steps (box tests + stack), leaf rounds, passes, waves,
  *  shade() inside the passes, next_ray() inside the passes}. */
 int  crt_renderer_get_section_profile(crt_renderer* r, unsigned long long* out7);
+/* The same plus word 7: ray_spheres() inside the passes (part of word 5); copies min(n, 8) words. */
+int  crt_renderer_get_section_profile_ex(crt_renderer* r, unsigned long long* out, int n);
 float* crt_renderer_linear_device_ptr(crt_renderer* r);   /* for RCCL reduce of the framebuffer */
 /* Bind the linear-sum framebuffer to caller-owned device memory of W*H*3 floats on the renderer's
  * device (e.g. a tensor the caller all-reduces with RCCL); NULL re-binds the internal buffer. */

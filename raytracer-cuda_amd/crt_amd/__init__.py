@@ -279,9 +279,9 @@ class Renderer:
 
     def section_profile(self) -> dict:
         """Shader-clock cycles per section of the last counting render (variant 4), summed over waves."""
-        a = (C.c_ulonglong * 7)()
-        check(_lib.hip().crt_renderer_get_section_profile(self.h, a), "get_section_profile")
-        return dict(zip(("cyc_regen", "cyc_step", "cyc_round", "passes", "waves", "cyc_shade", "cyc_next"),
+        a = (C.c_ulonglong * 8)()
+        check(_lib.hip().crt_renderer_get_section_profile_ex(self.h, a, 8), "get_section_profile_ex")
+        return dict(zip(("cyc_regen", "cyc_step", "cyc_round", "passes", "waves", "cyc_shade", "cyc_next", "cyc_sph"),
                         (int(v) for v in a)))
 
     def last_kernel_name(self) -> str:

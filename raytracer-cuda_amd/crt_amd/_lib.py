@@ -92,7 +92,7 @@ class WorkCounters(C.Structure):
 # exported symbol lists (checked by tests against include/*.h)
 HIP_SYMBOLS = [
     "crt_abi_version", "crt_last_error", "crt_device_count", "crt_scene_create", "crt_scene_create_ex", "crt_scene_get_stats", "crt_scene_compare", "crt_scene_compare_dump", "crt_scene_export",
-    "crt_renderer_set_stack_lds", "crt_renderer_get_section_profile",
+    "crt_renderer_set_stack_lds", "crt_renderer_get_section_profile", "crt_renderer_get_section_profile_ex",
     "crt_scene_destroy", "crt_renderer_create", "crt_renderer_destroy", "crt_renderer_init_rand",
     "crt_renderer_set_camera", "crt_renderer_render", "crt_renderer_resolve", "crt_renderer_render_frame",
     "crt_renderer_synchronize", "crt_renderer_read_linear", "crt_renderer_read_rgba8", "crt_renderer_read_rng",
@@ -146,6 +146,7 @@ def hip():
             "crt_scene_compare_dump": ([P, P, P, i32, i32, P, P, i32], i32),
             "crt_scene_export": ([P, P, P, P, P, P], i32), "crt_renderer_set_stack_lds": ([P, i32], i32),
             "crt_renderer_get_section_profile": ([P, P], i32),
+            "crt_renderer_get_section_profile_ex": ([P, P, i32], i32),
             "crt_scene_get_stats": ([P, P], i32),
             "crt_scene_destroy": ([P], None),
             "crt_renderer_create": ([i32, i32, i32, P], i32), "crt_renderer_destroy": ([P], None),

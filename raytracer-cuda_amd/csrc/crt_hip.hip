@@ -81,7 +81,8 @@ struct TraceCounts {
     uint32_t boxes, tris, spheres, step_slots, round_slots, trace_calls;
     // COUNT-mode section profile (variant 4; wave-uniform shader-clock cycles, s_memtime)
     uint64_t cyc_regen, cyc_step, cyc_round, passes;
-    uint64_t cyc_shade, cyc_next;   // inside the regen pass: shade(), next_ray(); the rest is ray init
+    uint64_t cyc_shade, cyc_next;   // inside the regen pass: ray_spheres() + shade(), next_ray(); the rest is ray init
+    uint64_t cyc_sph;               // of cyc_shade: the per-ray spheres (ray_spheres)
 };
 __device__ __forceinline__ uint64_t shader_clock() { return __builtin_amdgcn_s_memtime(); }
 
@@ -1101,7 +1102,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     C.lens = Cd.lens_radius;
     C.fw = (float)P.width;
     C.fh = (float)P.height;
-    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t wave_rays = 0;    // variant 8: rays of the wave (uniform); the other variants count per lane
 
     if (VARIANT == 0) {
@@ -1240,6 +1241,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     if (has_result)
                         ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
                                           sphere_inv(S.d, inv), closest, hit, sph_lds);
+                    if (COUNT) cnt.cyc_sph += shader_clock() - s0;
                     if (has_result) shade(S, P, hit, closest);
                     const uint64_t s1 = COUNT ? shader_clock() : 0;
                     live = next_ray(S, C, x, y, P.max_bounces);
@@ -1362,6 +1364,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             atomicAdd(&P.counters[12], 1ull);
             atomicAdd(&P.counters[13], (unsigned long long)cnt.cyc_shade);
             atomicAdd(&P.counters[14], (unsigned long long)cnt.cyc_next);
+            atomicAdd(&P.counters[7], (unsigned long long)cnt.cyc_sph);
         }
     }
     if (lane == 0) atomicAdd(&P.counters[0], (unsigned long long)wr);
@@ -1414,7 +1417,7 @@ __global__ __launch_bounds__(256) void crt_compare_kernel(CompareParams Q) {
     C.lens = Cd.lens_radius;
     C.fw = (float)P.width;
     C.fh = (float)P.height;
-    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long n_rank = 0, n_t = 0, n_bmiss = 0, n_amiss = 0;
     while (next_ray(S, C, x, y, P.max_bounces)) {
         ++S.rays;
@@ -2161,7 +2164,7 @@ struct crt_renderer {
     int n_cus = 0;
     int variant = 3;               // see crt_renderer_set_kernel_variant
     unsigned long long diag[3] = {0, 0, 0};
-    unsigned long long prof[7] = {0, 0, 0, 0, 0, 0, 0};   // COUNT-mode section profile (variant 4)
+    unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // COUNT-mode section profile (variant 4)
     int regen_threshold = 24;      // variants 2/3
     int regen_threshold_wide = 44; // variants 4/7/8 (measured: 40 for variant 4, profiles/r01d; 44-48 for 8, r01af)
     int crit_tiles = -1;           // variant 8: leading tiles of the cost order regenerating at crit_threshold; -1 = 4 per CU
@@ -2873,12 +2876,18 @@ int crt_renderer_get_counters(crt_renderer* R, crt_work_counters* out) {
     if (int rc = read_dev(R, c, R->d_counters, sizeof c)) return rc;
     R->diag[0] = c[5]; R->diag[1] = c[6] & ((1ull << 40) - 1); R->diag[2] = c[6] >> 40;
     for (int i = 0; i < 7; ++i) R->prof[i] = c[8 + i];
+    R->prof[7] = c[7];
     out->rays = c[0]; out->box_tests = c[1]; out->tri_tests = c[2]; out->sphere_tests = c[3]; out->paths = c[4];
     return take_device_error(R, c[ERR_WORD]);
 }
 int crt_renderer_get_section_profile(crt_renderer* R, unsigned long long* out7) {
     if (!R || !out7) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
     for (int i = 0; i < 7; ++i) out7[i] = R->prof[i];
+    return CRT_OK;
+}
+int crt_renderer_get_section_profile_ex(crt_renderer* R, unsigned long long* out, int n) {
+    if (!R || !out || n < 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    for (int i = 0; i < n && i < 8; ++i) out[i] = R->prof[i];
     return CRT_OK;
 }
 int crt_renderer_get_schedule_stats(crt_renderer* R, unsigned long long* out3) {
