@@ -99,16 +99,22 @@ struct Rng { uint32_t v0, v1, v2, v3, v4, d; };
 __device__ __forceinline__ uint32_t next_u32(Rng& s) {
     uint32_t t = s.v0 ^ (s.v0 >> 2);
     s.v0 = s.v1; s.v1 = s.v2; s.v2 = s.v3; s.v3 = s.v4;
-    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+    // (v4 ^ (v4 << 4)) ^ (t ^ (t << 1)): three of the four terms in one v_bitop3_b32 (0x96 = a ^ b ^ c)
+    s.v4 = __builtin_amdgcn_bitop3_b32(s.v4, s.v4 << 4, t, 0x96) ^ (t << 1);
     s.d += 362437u;
     return s.v4 + s.d;
 }
+// curand_uniform: (float)x * 2^-32 + 2^-33 (CURAND_2POW32_INV, two roundings in the reference).  (float)x has at most
+// 24 significant bits and x >= 1 or x == 0, so (float)x * 2^-32 is exact and the sum is the only rounding: one fma
+// gives the same bits as the multiply-then-add.
 __device__ __forceinline__ float uniform(Rng& s) {
-    const float inv = 2.3283064e-10f;   // CURAND_2POW32_INV
-    return (float)next_u32(s) * inv + (inv / 2.0f);
+    return __builtin_fmaf((float)next_u32(s), 0x1p-32f, 0x1p-33f);
 }
-// Utility.cuh:18-21: min + (max - min) * U, here min=-1, max=1.
-__device__ __forceinline__ float rand_pm1(Rng& s) { return -1.0f + 2.0f * uniform(s); }
+// Utility.cuh:18-21: min + (max - min) * U, here min=-1, max=1: -1 + 2 * fl(X * 2^-32 + 2^-33).  Doubling is exact, so
+// 2 * U = fl(X * 2^-31 + 2^-32), again one exact product and one rounding: fma, then the reference's subtraction.
+__device__ __forceinline__ float rand_pm1(Rng& s) {
+    return -1.0f + __builtin_fmaf((float)next_u32(s), 0x1p-31f, 0x1p-32f);
+}
 
 __device__ __forceinline__ V3 rand_unit_vector(Rng& s) {   // Utility.cuh:45-53, :73-76
     V3 p;
