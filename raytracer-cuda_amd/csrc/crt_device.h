@@ -70,6 +70,14 @@ __device__ __forceinline__ float recip_exact_any(float x) {
     return (a >= RCP_FAST_MIN && a < RCP_FAST_MAX) ? rcp_newton(x) : 1.0f / x;
 }
 
+// 1.f / x, bit for bit, by rcp_newton when every active lane's |x| lies in the exhaustively verified range (a
+// wave-uniform branch, so a wave never runs both sequences), else by IEEE division.
+__device__ __forceinline__ float recip_exact_wave(float x) {
+    const float a = fabsf(x);
+    if (__builtin_amdgcn_ballot_w64(!(a >= RCP_FAST_MIN && a < RCP_FAST_MAX)) == 0) return rcp_newton(x);
+    return 1.0f / x;
+}
+
 struct V3 { float x, y, z; };
 
 __device__ __forceinline__ V3 v3(float a, float b, float c) { return V3{a, b, c}; }
@@ -83,7 +91,8 @@ __device__ __forceinline__ V3 cross(V3 u, V3 v) {                               
     return v3(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
 }
 __device__ __forceinline__ float len2(V3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }            // :95
-__device__ __forceinline__ V3 unit(V3 v) { return (1.0f / sqrtf(len2(v))) * v; }                     // :201,:213
+// Vec3::unit: (1 / length) * v, the reciprocal exact (recip_exact_wave; -0.5 %, profiles/r02s)
+__device__ __forceinline__ V3 unit(V3 v) { return recip_exact_wave(sqrtf(len2(v))) * v; }             // :201,:213
 __device__ __forceinline__ V3 reflect(V3 v, V3 n) { return v - (2.0f * dot(v, n)) * n; }              // :225
 __device__ __forceinline__ V3 refract(V3 uv, V3 n, float eta) {                                        // :229
     float cos_theta = fminf(dot(-uv, n), 1.0f);

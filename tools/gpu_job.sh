@@ -9,6 +9,8 @@
 #                                         tools/build_profile_lib.sh), N alternating A B rounds of bench.py ARGS
 #   tools/gpu_job.sh pmc OUT [ARGS..]     rocprofv3 --pmc passes (tools/pmc.sh) over one bench frame
 #   tools/gpu_job.sh l1 OUT               vector-L1 calibration micro-benchmark (tools/probes/l1_probe.hip) + PMC
+#   tools/gpu_job.sh libs OUT N LIB ...     N interleaved rounds of the default bench over the in-tree library (A) and
+#                                         each LIB (paths to libcrt_hip.so builds, e.g. from tools/build_profile_lib.sh)
 #   tools/gpu_job.sh sweep OUT N "label=ARGS" ...
 #                                         N interleaved rounds of bench.py, one run per "label=ARGS" set (the args
 #                                         after '=' split on spaces); one log per label and round
@@ -48,6 +50,18 @@ l1)
   cd /tmp && export TMPDIR=/tmp
   timeout -s KILL 120 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES TCP_PENDING_STALL_CYCLES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE \
       --output-format csv -d $R/$OUT/pmc -o l1 -- $R/tools/probes/l1_probe > $R/$OUT/l1_pmc.log 2>&1
+  ;;
+libs)
+  N=$1; shift
+  for i in $(seq 1 $N); do
+    timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-count --no-parity > $R/$OUT/A_$i.log 2>&1
+    echo "A round $i: $(grep -o '"render_kernel_ms_avg": [0-9.]*' $R/$OUT/A_$i.log)"
+    for lib in "$@"; do
+      label=$(basename $(dirname $lib))
+      CRT_HIP_LIB=$R/$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-count --no-parity > $R/$OUT/${label}_$i.log 2>&1
+      echo "$label round $i: $(grep -o '"render_kernel_ms_avg": [0-9.]*' $R/$OUT/${label}_$i.log)"
+    done
+  done
   ;;
 sweep)
   N=$1; shift
