@@ -42,8 +42,8 @@ namespace crt {
 //             outward = (1/radius) * (hp - center) at the hit (Sphere.cuh:44), 1/radius in the third float4
 //   kind & 15 = SHADE_LAMBERT / _METAL / _DIELECTRIC / _LIGHT / _NOEMIT (unknown type: emit 0) /
 //               _INVALID (material index out of range: the same-ray bounce of CUDAKernels.h:127)
-//   payload: lambertian (albedo.xyz, 0)  metal (albedo.xyz, min(roughness, 1))  dielectric (ior, 0, 0, 0)
-//            light (emission.xyz, 0)
+//   payload: lambertian (albedo.xyz, 0)  metal (albedo.xyz, min(roughness, 1))  light (emission.xyz, 0)
+//            dielectric (ior, 1/ior, r0(1/ior), r0(ior)) with Schlick's r0(ri) = ((1 - ri) / (1 + ri))^2
 constexpr uint32_t SHADE_LAMBERT = 0, SHADE_METAL = 1, SHADE_DIELECTRIC = 2, SHADE_LIGHT = 3, SHADE_NOEMIT = 4,
                    SHADE_INVALID = 5, SHADE_SPHERE = 16;
 constexpr int NODE_MESH_INNER = -1;
@@ -113,17 +113,14 @@ __device__ __forceinline__ uint32_t next_u32(Rng& s) {
     s.d += 362437u;
     return s.v4 + s.d;
 }
-// curand_uniform: (float)x * 2^-32 + 2^-33 (CURAND_2POW32_INV, two roundings in the reference).  (float)x has at most
-// 24 significant bits and x >= 1 or x == 0, so (float)x * 2^-32 is exact and the sum is the only rounding: one fma
-// gives the same bits as the multiply-then-add.
-__device__ __forceinline__ float uniform(Rng& s) {
-    return __builtin_fmaf((float)next_u32(s), 0x1p-32f, 0x1p-33f);
-}
-// Utility.cuh:18-21: min + (max - min) * U, here min=-1, max=1: -1 + 2 * fl(X * 2^-32 + 2^-33).  Doubling is exact, so
-// 2 * U = fl(X * 2^-31 + 2^-32), again one exact product and one rounding: fma, then the reference's subtraction.
-__device__ __forceinline__ float rand_pm1(Rng& s) {
-    return -1.0f + __builtin_fmaf((float)next_u32(s), 0x1p-31f, 0x1p-32f);
-}
+// curand_uniform: (float)x * 2^-32 + 2^-33 (CURAND_2POW32_INV and half of it).  Both constants are VOP2 literals, so
+// no register holds them (an fma form, one rounding of the same exact product, needs both in VGPRs on gfx950 and
+// measured +1.3 % through register pressure, profiles/r02t).
+__device__ __forceinline__ float uniform(Rng& s) { return (float)next_u32(s) * 0x1p-32f + 0x1p-33f; }
+// Utility.cuh:18-21: min + (max - min) * U, here min=-1, max=1: -1 + 2 * fl(X * 2^-32 + 2^-33).  (float)x has at most 24
+// significant bits, so X * 2^-32 is exact and doubling commutes with the rounding: 2 * U = fl(X * 2^-31 + 2^-32), one
+// multiply fewer than the literal restatement, the same bits.
+__device__ __forceinline__ float rand_pm1(Rng& s) { return -1.0f + ((float)next_u32(s) * 0x1p-31f + 0x1p-32f); }
 
 __device__ __forceinline__ V3 rand_unit_vector(Rng& s) {   // Utility.cuh:45-53, :73-76
     V3 p;
@@ -138,10 +135,10 @@ __device__ __forceinline__ V3 rand_unit_vector(Rng& s) {   // Utility.cuh:45-53,
     return unit(p);
 }
 
-// Material.cuh:132-137 with pow(float,int) restated as exponentiation by squaring.
-__device__ __forceinline__ float schlick(float cosine, float ref_idx) {
-    float r0 = (1 - ref_idx) / (1 + ref_idx);
-    r0 = r0 * r0;
+// Material.cuh:132-137 with pow(float,int) restated as exponentiation by squaring.  r0 = ((1 - ref_idx) /
+// (1 + ref_idx))^2 depends on the material and the face only: the shading record carries it (schlick_r0 in
+// crt_hip.hip's shading_records, IEEE f32 on the host, the same bits), so a hit pays no division for it.
+__device__ __forceinline__ float schlick_r0(float cosine, float r0) {
     float a = 1 - cosine;
     float r = 1.0f * a;          // e = 5: bit0
     a = a * a;                   // e = 2

@@ -968,6 +968,22 @@ __device__ __forceinline__ bool next_ray(PathState& S, const CamRegs& C, int x, 
     }
 }
 
+// Dielectric::scatter's total-internal-reflection test in double, as the reference computes it (Material.cuh:115-118):
+//   cannot = RN(ri * RN(sqrt(y))) > 1,   y = RN(1 - c * c)   (c * c is exact in double: two 24-bit factors).
+// sqrt and the product are correctly rounded and monotone, so ri^2 * y decides the outcome unless it is within a hair
+// of 1.  z = RN(RN(ri * ri) * y) is within a relative 2^-52 of ri^2 * y.  If z > 1 + 2^-40, then ri * sqrt(y) >
+// 1 + 2^-43, and the two roundings (a relative 2^-53 each) keep RN(ri * RN(sqrt(y))) above 1 + 2^-53, so it rounds
+// above 1.  If z < 1 - 2^-40, the product stays below 1.  Only a wave with a lane in between (or a NaN) runs the
+// reference's f64 sqrt; the f64 sqrt sequence is otherwise the most expensive part of the glass shading.
+__device__ __forceinline__ bool cannot_refract_exact(float cos_theta, float ri) {
+    const double c = cos_theta, r = ri;
+    const double y = __builtin_fma(-c, c, 1.0);          // == RN(1.0 - c * c): the product is exact
+    const double z = (r * r) * y;
+    const bool above = z > 1.0 + 0x1p-40, below = z < 1.0 - 0x1p-40;
+    if (__builtin_amdgcn_ballot_w64(!(above || below)) == 0) return above;
+    return r * sqrt(y) > 1.0;
+}
+
 // Phase 3: material scatter / emit / sky (CUDAKernels.h:123-142, Material.cuh:66-146).  The hit's normal and
 // material come from its shading record (crt_device.h): one pair of independent loads per hit.
 __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int hit_rank, float t) {
@@ -1015,14 +1031,13 @@ __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int h
             S.need_new = true;
         }
     } else if (code == SHADE_DIELECTRIC) {               // :109-128
-        const float ior = m.x;
-        const float ri = front ? (1.0f / ior) : ior;
+        const float ri = front ? m.y : m.x;              // 1.0f / ior (front face) or ior, from the shading record
+        const float r0 = front ? m.z : m.w;              // Schlick's r0 for that ri
         const V3 ud = unit(S.d);
-        const double cos_theta = fminf(dot(-ud, n), 1.0f);
-        const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
-        const bool cannot_refract = (double)ri * sin_theta > 1.0;
+        const float cos_theta = fminf(dot(-ud, n), 1.0f);
+        const bool cannot_refract = cannot_refract_exact(cos_theta, ri);
         V3 dir;
-        if (cannot_refract || schlick((float)cos_theta, ri) > uniform(S.s))
+        if (cannot_refract || schlick_r0(cos_theta, r0) > uniform(S.s))
             dir = reflect(ud, n);
         else
             dir = refract(ud, n, ri);
@@ -2288,7 +2303,15 @@ static std::vector<float4> shading_records(const std::vector<int>& rank_code, co
                     code = SHADE_METAL;
                     pay = make_float4(M.albedo[0], M.albedo[1], M.albedo[2], M.roughness < 1.f ? M.roughness : 1.f);
                     break;
-                case CRT_DIELECTRIC: code = SHADE_DIELECTRIC; pay = make_float4(M.ior, 0.f, 0.f, 0.f); break;
+                case CRT_DIELECTRIC: {
+                    // Material.cuh:113 ri = front ? 1.0f / ior : ior, and Schlick's r0 = ((1 - ri) / (1 + ri))^2
+                    // (:133-134) for both faces, in IEEE f32 as the device would compute them per hit
+                    code = SHADE_DIELECTRIC;
+                    auto r0 = [](float r) { const float x = (1 - r) / (1 + r); return x * x; };
+                    const float inv = 1.0f / M.ior;
+                    pay = make_float4(M.ior, inv, r0(inv), r0(M.ior));
+                    break;
+                }
                 case CRT_DIFFUSE_LIGHT:
                     code = SHADE_LIGHT;
                     pay = make_float4(M.emission[0], M.emission[1], M.emission[2], 0.f);
