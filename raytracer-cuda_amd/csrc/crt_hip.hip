@@ -812,6 +812,12 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
             const int hi = (int)((ends >> (8u * last)) & 0xffu);
             leaf_n = hi - lo;
             leaf_first = __float_as_int(mf.z) + lo;
+            // the span must lie inside the primitive array: checked here once per lane and step instead of per pair
+            // in the leaf rounds (-0.7 %, profiles/r02v); a corrupt node reports through P.err and tests nothing
+            if ((unsigned)(leaf_first + leaf_n) > (unsigned)P.n_prims) {
+                atomicOr(P.err, 1u);
+                leaf_n = 0;
+            }
         }
         uint32_t k[4];
 #pragma unroll
@@ -881,17 +887,13 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         const int j = base + lane;
         if (j < total) {
             const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
-            const int p = __float_as_int(r1.w) + (j - L.prefix[owner]);
+            const int p = __float_as_int(r1.w) + (j - L.prefix[owner]);   // inside the owner's checked span
             if (COUNT) cnt.tris++;
-            if ((unsigned)p < (unsigned)P.n_prims) {
-                int rank;
-                const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
-                                          P.tree_spheres != 0);
-                if (t >= 0.f)
-                    atomicMin(&L.key[owner], ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank));
-            } else {
-                atomicOr(P.err, 1u);
-            }
+            int rank;
+            const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
+                                      P.tree_spheres != 0);
+            if (t >= 0.f)
+                atomicMin(&L.key[owner], ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank));
         }
         carry = __builtin_amdgcn_readlane(owner1, 63);
         wave_sync();
@@ -962,7 +964,7 @@ __device__ __forceinline__ bool next_ray(PathState& S, const CamRegs& C, int x, 
                 S.need_new = true;
                 continue;
             }
-            S.thr = (1 / p) * S.thr;
+            S.thr = recip_exact_wave(p) * S.thr;   // 1 / p, exact (crt_device.h)
         }
         return true;
     }
