@@ -189,6 +189,10 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
     return hit;
 }
 
+// Lanes of the wave (active lanes only) whose predicate holds.  HIP's __ballot widens the predicate to an int and
+// compares it again (two VALU per ballot); the builtin takes the compare's lane mask as it is.
+__device__ __forceinline__ uint64_t wave_ballot(bool pred) { return __builtin_amdgcn_ballot_w64(pred); }
+
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
     return x;
@@ -304,7 +308,8 @@ __device__ __forceinline__ const float4* rec_at(const float4* base, uint32_t byt
 // planes are three cache lines per triangle where the 48-B record mostly sits in one, profiles/r02c.)
 __device__ __forceinline__ float prim_test(const float4* __restrict__ prims, int p, V3 o, V3 d, float tmax, int& rank,
                                            bool tree_spheres = true) {
-    const float4* r = rec_at(prims, (uint32_t)p * 48u);
+    // 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate): the 4-wide tree holds < 2^24 primitives (emit4)
+    const float4* r = rec_at(prims, __umul24((uint32_t)p, 48u));
     const float4 f0 = r[0], f1 = r[1], f2 = r[2];
     // keep the unused word: the third row then loads as one dwordx4 instead of a dword + a dwordx2 (one vector-L1
     // lookup set less per pair; -0.7 %, profiles/r02s)
@@ -354,7 +359,7 @@ __device__ int trace_coop(const float4* __restrict__ nodes, const float4* __rest
     L.ray0[lane] = make_float4(o.x, o.y, o.z, d.x);
     L.owner_at[lane] = 0;      // owner + 1, 0 = none
     if (COUNT) cnt.trace_calls++;
-    while (__ballot(node < n_nodes)) {
+    while (wave_ballot(node < n_nodes)) {
         if (COUNT) cnt.step_slots++;        // one traversal step of the wave (x64 lanes)
         int leaf_n = 0, leaf_first = 0;
         if (node < n_nodes) {
@@ -386,7 +391,7 @@ __device__ int trace_coop(const float4* __restrict__ nodes, const float4* __rest
             }
             node = next;
         }
-        if (!__ballot(leaf_n > 0)) continue;
+        if (!wave_ballot(leaf_n > 0)) continue;
         const int incl = wave_inclusive_scan(leaf_n, lane);
         const int total = __builtin_amdgcn_readlane(incl, 63);
         const int pfx = incl - leaf_n;
@@ -483,7 +488,7 @@ __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, 
             pB = nodes[nbase + 2 * next + 1];
         }
     }
-    if (!__ballot(leaf_n > 0)) return;
+    if (!wave_ballot(leaf_n > 0)) return;
     const int incl = wave_inclusive_scan(leaf_n, lane);
     const int total = __builtin_amdgcn_readlane(incl, 63);
     const int pfx = incl - leaf_n;
@@ -806,7 +811,12 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
         for (int s = 0; s < 4; ++s) hm |= w.hit[s] ? (1u << s) : 0u;
         const uint32_t lm = hm & (0xfu << n_int);
         if (lm) {
-            const uint32_t ends = counts * 0x01010101u;
+            // counts * 0x01010101 (byte-wise running sums) as shift-adds: a 32-bit multiply is quarter rate (the empty
+            // asm keeps the compiler from folding the shifts back into one)
+            uint32_t c2 = counts + (counts << 8);
+            __asm__("" : "+v"(c2));
+            uint32_t ends = c2 + (c2 << 16);
+            __asm__("" : "+v"(ends));
             const uint32_t first = (uint32_t)__builtin_ctz(lm), last = 31u - (uint32_t)__builtin_clz(lm);
             const int lo = (int)(((ends << 8) >> (8u * first)) & 0xffu);
             const int hi = (int)((ends >> (8u * last)) & 0xffu);
@@ -862,7 +872,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
     node_step4<COUNT>(P, o, inv, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
     const uint64_t c1 = COUNT ? shader_clock() : 0;
     if (COUNT) cnt.cyc_step += c1 - c0;
-    if (!__ballot(leaf_n > 0)) return;
+    if (!wave_ballot(leaf_n > 0)) return;
     const int incl = wave_inclusive_scan(leaf_n, lane);
     const int total = __builtin_amdgcn_readlane(incl, 63);
     const int pfx = incl - leaf_n;
@@ -887,7 +897,10 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         const int j = base + lane;
         if (j < total) {
             const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
-            const int p = __float_as_int(r1.w) + (j - L.prefix[owner]);   // inside the owner's checked span
+            // the prefix address from its own base: derived from ray1's, the compiler builds it with a 64-bit multiply
+            int owner_p = owner;
+            __asm__("" : "+v"(owner_p));
+            const int p = __float_as_int(r1.w) + (j - L.prefix[owner_p]);   // inside the owner's checked span
             if (COUNT) cnt.tris++;
             int rank;
             const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
@@ -995,7 +1008,7 @@ __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int h
         S.need_new = true;
         return;
     }
-    const float4* R = P.shade + 3 * (size_t)hit_rank;
+    const float4* R = P.shade + 3u * (uint32_t)hit_rank;   // 32-bit index (ranks < 2^30): no 64-bit multiply
     const float4 r0 = R[0], m = R[1];
     const uint32_t kind = __float_as_uint(r0.w);
     const V3 hp = S.o + t * S.d;                         // Ray::pointAtDistance
@@ -1154,8 +1167,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         L.owner_at[lane] = 0;
         for (;;) {
             const bool parked = live && node < 0;
-            const int n_parked = __popcll(__ballot(parked));
-            const int n_live = __popcll(__ballot(live));
+            const int n_parked = __popcll(wave_ballot(parked));
+            const int n_live = __popcll(wave_ballot(live));
             const uint64_t c0 = COUNT ? shader_clock() : 0;
             if (n_parked >= P.regen_threshold || n_parked == n_live) {
                 if (COUNT) cnt.passes++;
@@ -1176,7 +1189,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     have = false;
                 }
                 while (!exhausted) {                // lanes without a pixel take the next slots
-                    const uint64_t need = __ballot(!have);
+                    const uint64_t need = wave_ballot(!have);
                     if (need == 0) break;
                     if (used >= 64u) {
                         uint32_t b = 0;
@@ -1227,7 +1240,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                     if (COUNT) cnt.trace_calls++;
                 }
-                if (!__ballot(live)) break;      // the queue is empty and every lane is done
+                if (!wave_ballot(live)) break;      // the queue is empty and every lane is done
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
             traverse_step4<COUNT>(P, S.o, S.d, inv, node, sp, closest, hit, cnt, L, stk, lane, (size_t)ppix, n_pix);
@@ -1238,7 +1251,11 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         uint32_t* stk = stack_lds + wave * SD * 64;
         const float INF = __builtin_inff();
         const size_t n_pix = (size_t)P.width * P.height;
-        bool live = true, has_result = false;
+        // Lane masks instead of per-lane bools for the per-step tests: a ballot of a bool the compiler keeps as a lane
+        // mask costs two VALU (widen, compare), a ballot of a compare none.  Every lane starts live (a pixel without
+        // samples ends at the first pass); after a pass the live lanes are exactly those with a ray (has_result).
+        uint64_t live_mask = wave_ballot(true);
+        bool has_result = false;
         int node = -1, sp = 0, hit = -1;
         float closest = INF;
         V3 inv = v3(0.f, 0.f, 0.f);
@@ -1247,14 +1264,14 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
         const int regen_t = (TILED && (int)blockIdx.x < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
         for (;;) {
-            const bool parked = live && node < 0;
-            const int n_parked = __popcll(__ballot(parked));
-            const int n_live = __popcll(__ballot(live));
+            const uint64_t parked_mask = live_mask & wave_ballot(node < 0);
+            const int n_parked = __popcll(parked_mask);
+            const int n_live = __popcll(live_mask);
             if (n_live == 0) break;
             const uint64_t c0 = COUNT ? shader_clock() : 0;
             if (n_parked >= regen_t || n_parked == n_live) {
                 if (COUNT) cnt.passes++;
-                if (parked) {
+                if (__builtin_amdgcn_inverse_ballot_w64(parked_mask)) {
                     const uint64_t s0 = COUNT ? shader_clock() : 0;
                     // (loading the shading record before this sphere test, to overlap its latency, measured +0.7 %:
                     // profiles/r01ar)
@@ -1264,7 +1281,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     if (COUNT) cnt.cyc_sph += shader_clock() - s0;
                     if (has_result) shade(S, P, hit, closest);
                     const uint64_t s1 = COUNT ? shader_clock() : 0;
-                    live = next_ray(S, C, x, y, P.max_bounces);
+                    const bool live = next_ray(S, C, x, y, P.max_bounces);
                     if (COUNT) {
                         const uint64_t s2 = shader_clock();
                         cnt.cyc_shade += s1 - s0;
@@ -1287,8 +1304,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         if (COUNT) cnt.trace_calls++;
                     }
                 }
+                live_mask = wave_ballot(has_result);
                 // variant 8 counts the wave's rays in a scalar (one VGPR less in the hot loop)
-                if (TILED) wave_rays += (uint32_t)__popcll(__ballot(parked && has_result));
+                if (TILED) wave_rays += (uint32_t)__popcll(parked_mask & live_mask);
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
             traverse_step4<COUNT>(P, S.o, S.d, inv, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
@@ -1308,8 +1326,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         L.owner_at[lane] = 0;      // owner + 1, 0 = none
         for (;;) {
             const bool parked = live && node >= P.n_nodes;
-            const int n_parked = __popcll(__ballot(parked));
-            const int n_live = __popcll(__ballot(live));
+            const int n_parked = __popcll(wave_ballot(parked));
+            const int n_live = __popcll(wave_ballot(live));
             if (n_live == 0) break;
             if (n_parked >= P.regen_threshold || n_parked == n_live) {
                 if (parked) {
@@ -1340,7 +1358,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         bool live = true;
         for (;;) {
             if (live) live = next_ray(S, C, x, y, P.max_bounces);
-            if (!__ballot(live)) break;
+            if (!wave_ballot(live)) break;
             float t;
             const int hit = trace_coop<COUNT>(P.nodes, P.prims, P.n_nodes, layout_base(S.d, P.n_layouts, P.n_nodes),
                                               P.n_prims, P.err, S.o, S.d, live, t, cnt, lds[wave], lane);
@@ -2073,7 +2091,8 @@ private:
                     rank_code[F.rank_of[src]] = its[i].sphere ? (SPHERE_BIT | np) : np;
                 }
             }
-            if (prims.size() / 3 >= (size_t)SPHERE_BIT) { err = "too many primitives"; return false; }
+            // prim_test addresses a record as __umul24(index, 48): the 4-wide tree holds fewer than 2^24 primitives
+            if (prims.size() / 3 >= ((size_t)1 << 24)) { err = "the 4-wide tree holds at most 2^24 - 1 primitives"; return false; }
             // node_step4 takes the leaf span from counts * 0x01010101 (byte-wise running sums)
             if (total_leaf > 255) { err = "leaf children of one node hold more than 255 primitives"; return false; }
             float row[6][4];
