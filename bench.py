@@ -91,6 +91,8 @@ def parse():
     ap.add_argument("--kernel-variant", type=int, default=None, help="render-kernel variant (default: library's)")
     ap.add_argument("--regen-threshold", type=int, default=None,
                     help="parked lanes before a regeneration pass (default: the library's, 44 for 4-wide scenes)")
+    ap.add_argument("--occupancy", type=int, default=None,
+                    help="render-kernel occupancy target in waves per SIMD (default: the library's, 6 for 4-wide scenes)")
     ap.add_argument("--critical-tiles", type=int, default=None,
                     help="variant 8: leading tiles of the cost order that regenerate sooner (default: library's)")
     ap.add_argument("--critical-lanes", type=int, default=16, help="their regeneration threshold")
@@ -292,6 +294,8 @@ def main():
         r.set_kernel_variant(args.kernel_variant)
     if args.regen_threshold is not None:
         r.set_regen_threshold(args.regen_threshold)
+    if args.occupancy is not None:
+        r.set_occupancy_target(args.occupancy)
     if args.critical_tiles is not None:
         r.set_critical_tiles(args.critical_tiles, args.critical_lanes)
     r.set_camera(cam)
