@@ -11,6 +11,8 @@
 #   tools/gpu_job.sh l1 OUT               vector-L1 calibration micro-benchmark (tools/probes/l1_probe.hip) + PMC
 #   tools/gpu_job.sh libs OUT N LIB ...     N interleaved rounds of the default bench over the in-tree library (A) and
 #                                         each LIB (paths to libcrt_hip.so builds, e.g. from tools/build_profile_lib.sh)
+#   tools/gpu_job.sh viewer OUT            the interactive loop (bin/crt_viewer): 600 frames of 1 spp at 2560x1440, still
+#                                         and orbiting, rebuilt BVH, one JSON line each
 #   tools/gpu_job.sh sweep OUT N "label=ARGS" ...
 #                                         N interleaved rounds of bench.py, one run per "label=ARGS" set (the args
 #                                         after '=' split on spaces); one log per label and round
@@ -61,6 +63,12 @@ libs)
       CRT_HIP_LIB=$R/$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-count --no-parity > $R/$OUT/${label}_$i.log 2>&1
       echo "$label round $i: $(grep -o '"render_kernel_ms_avg": [0-9.]*' $R/$OUT/${label}_$i.log)"
     done
+  done
+  ;;
+viewer)
+  F=$(CRT_NO_TORCH=1 python3 -c "import sys; sys.path.insert(0, 'raytracer-cuda_amd'); from crt_amd import assets; print(' '.join(map(str, assets.scene_files('cornell_bunny'))))")
+  for s in still orbit; do
+    timeout -k 10 120 raytracer-cuda_amd/bin/crt_viewer -frames 600 -script $s -bvh rebuilt $F > $R/$OUT/viewer_${s}_rebuilt.json
   done
   ;;
 sweep)
