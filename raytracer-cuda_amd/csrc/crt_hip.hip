@@ -253,7 +253,6 @@ struct WaveLds {
 
 // Möller–Trumbore (Mesh.cuh:266-308) on a triangle record; returns t or -1 when rejected (any accepted
 // t >= 0.001).
-typedef float pf2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float tri_test_rec(float4 f0, float4 f1, float4 f2, V3 o, V3 d, float tmax) {
     const V3 e1 = v3(f0.w, f1.x, f1.y);
     const V3 e2 = v3(f1.z, f1.w, f2.x);
@@ -548,8 +547,8 @@ struct Wide4 {
     bool hit[4];
 };
 
-// Slab test of the four child boxes against [0.001, tmax] in packed f32: lo * inv - o * inv as one v_pk_fma_f32 per
-// pair of planes (half the VALU of (lo - o) * inv; measured -2.1 %, profiles/r01at).  Its error, about ulp(o) * |inv|
+// Slab test of the four child boxes against [0.001, tmax]: plane * inv - o * inv as one fma per plane (one operation
+// where (lo - o) * inv takes two; measured -2.1 %, profiles/r01at).  Its error, about ulp(o) * |inv|
 // in t, is of the same order as that of (lo - o) * inv and far inside the boxes' 1e-5 * max(1, |coord|) padding
 // (DESIGN.md §2b).  inv must be finite AND o * inv / lo * inv must not overflow: an infinite product makes
 // lo * inv - o * inv = inf - inf = NaN on a plane, and the min/max would then cull a box the ray runs inside of.
@@ -589,23 +588,18 @@ __device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ nodes, ui
     const float4 nxr = *rec_at(nodes, b ^ sx), fxr = *rec_at(nodes, b ^ (16u ^ sx));
     const float4 nyr = *rec_at(nodes, b ^ (32u ^ sy)), fyr = *rec_at(nodes, b ^ (48u ^ sy));
     const float4 nzr = *rec_at(nodes, b ^ (64u ^ sz)), fzr = *rec_at(nodes, b ^ (80u ^ sz));
-    const pf2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+    // one v_fma_f32 per plane: a v_pk_fma_f32 costs the SIMD the same cycles as two (MI355X_MICROARCH.md) and needs
+    // {inv, inv} / {-o*inv, -o*inv} register pairs, which made the persistent variant 7 spill in this step (the
+    // scalar form: variant 8 -1.7 %, variant 7 -18 %, profiles/r02aa)
     const float nx = -(o.x * inv.x), ny = -(o.y * inv.y), nz = -(o.z * inv.z);
-    const pf2 ox = {nx, nx}, oy = {ny, ny}, oz = {nz, nz};
-    const pf2 ax0 = __builtin_elementwise_fma((pf2){nxr.x, nxr.y}, ix, ox), ax1 = __builtin_elementwise_fma((pf2){nxr.z, nxr.w}, ix, ox);
-    const pf2 bx0 = __builtin_elementwise_fma((pf2){fxr.x, fxr.y}, ix, ox), bx1 = __builtin_elementwise_fma((pf2){fxr.z, fxr.w}, ix, ox);
-    const pf2 ay0 = __builtin_elementwise_fma((pf2){nyr.x, nyr.y}, iy, oy), ay1 = __builtin_elementwise_fma((pf2){nyr.z, nyr.w}, iy, oy);
-    const pf2 by0 = __builtin_elementwise_fma((pf2){fyr.x, fyr.y}, iy, oy), by1 = __builtin_elementwise_fma((pf2){fyr.z, fyr.w}, iy, oy);
-    const pf2 az0 = __builtin_elementwise_fma((pf2){nzr.x, nzr.y}, iz, oz), az1 = __builtin_elementwise_fma((pf2){nzr.z, nzr.w}, iz, oz);
-    const pf2 bz0 = __builtin_elementwise_fma((pf2){fzr.x, fzr.y}, iz, oz), bz1 = __builtin_elementwise_fma((pf2){fzr.z, fzr.w}, iz, oz);
-    const float ax[4] = {ax0.x, ax0.y, ax1.x, ax1.y}, bx[4] = {bx0.x, bx0.y, bx1.x, bx1.y};
-    const float ay[4] = {ay0.x, ay0.y, ay1.x, ay1.y}, by[4] = {by0.x, by0.y, by1.x, by1.y};
-    const float az[4] = {az0.x, az0.y, az1.x, az1.y}, bz[4] = {bz0.x, bz0.y, bz1.x, bz1.y};
     Wide4 w;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        const float t0 = fmaxf(fmaxf(ax[s], ay[s]), fmaxf(az[s], 0.001f));
-        const float t1 = fminf(fminf(bx[s], by[s]), fminf(bz[s], tmax));
+        const float ax = __builtin_fmaf((&nxr.x)[s], inv.x, nx), bx = __builtin_fmaf((&fxr.x)[s], inv.x, nx);
+        const float ay = __builtin_fmaf((&nyr.x)[s], inv.y, ny), by = __builtin_fmaf((&fyr.x)[s], inv.y, ny);
+        const float az = __builtin_fmaf((&nzr.x)[s], inv.z, nz), bz = __builtin_fmaf((&fzr.x)[s], inv.z, nz);
+        const float t0 = fmaxf(fmaxf(ax, ay), fmaxf(az, 0.001f));
+        const float t1 = fminf(fminf(bx, by), fminf(bz, tmax));
         w.tmin[s] = t0;
         w.hit[s] = t0 < t1;
     }
@@ -654,37 +648,40 @@ __device__ __forceinline__ bool sphere_beyond(float qa, float hb, float disc, fl
 }
 
 // Two spheres at once (data from the kernel arguments): the reference box tests and the discriminant
-// arithmetic in packed f32 (IEEE per half, the reference's operation order: (x*x + y*y) + z*z), roots and
-// divisions per sphere.
+// arithmetic (IEEE, the reference's operation order: (x*x + y*y) + z*z), roots and divisions per sphere.  In scalar
+// f32: the packed form (v_pk_*) takes the same SIMD cycles and its register pairs cost the hot loop two spilled
+// VGPRs (-1.2 % without, profiles/r02ab).
 template <bool LATE = false>
 __device__ __forceinline__ void ray_spheres2(const float* sa, const float* sb, V3 o, V3 d, V3 inv,
                                              float& closest, int& hit) {
-    const pf2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
-    const pf2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
-    const pf2 t0x = ((pf2){sa[5], sb[5]} - ox) * ix, t1x = ((pf2){sa[8], sb[8]} - ox) * ix;
-    const pf2 t0y = ((pf2){sa[6], sb[6]} - oy) * iy, t1y = ((pf2){sa[9], sb[9]} - oy) * iy;
-    const pf2 t0z = ((pf2){sa[7], sb[7]} - oz) * iz, t1z = ((pf2){sa[10], sb[10]} - oz) * iz;
+    const float* sp[2] = {sa, sb};
     bool reach[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-        float tmin = fmaxf(fmaxf(fminf(t0x[s], t1x[s]), fminf(t0y[s], t1y[s])), fminf(t0z[s], t1z[s]));
-        float tmax = fminf(fminf(fmaxf(t0x[s], t1x[s]), fmaxf(t0y[s], t1y[s])), fmaxf(t0z[s], t1z[s]));
+        const float* q = sp[s];
+        const float t0x = (q[5] - o.x) * inv.x, t1x = (q[8] - o.x) * inv.x;
+        const float t0y = (q[6] - o.y) * inv.y, t1y = (q[9] - o.y) * inv.y;
+        const float t0z = (q[7] - o.z) * inv.z, t1z = (q[10] - o.z) * inv.z;
+        float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+        float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
         tmin = fmaxf(tmin, 0.001f);
         reach[s] = !(tmax <= tmin);
     }
     if (!(reach[0] || reach[1])) return;
-    const pf2 ocx = ox - (pf2){sa[0], sb[0]}, ocy = oy - (pf2){sa[1], sb[1]}, ocz = oz - (pf2){sa[2], sb[2]};
     const float qa = dot(d, d);
-    const pf2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
-    const pf2 hb = (ocx * dx + ocy * dy) + ocz * dz;
-    const pf2 qc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - (pf2){sa[3], sb[3]};
-    const pf2 qa2 = {qa, qa};
-    const pf2 disc = hb * hb - qa2 * qc;
-    const float ta = reach[0] && !(LATE && sphere_beyond(qa, hb.x, disc.x, closest)) ? sphere_root(qa, hb.x, disc.x) : -1.f;
-    const float tb = reach[1] && !(LATE && sphere_beyond(qa, hb.y, disc.y, closest)) ? sphere_root(qa, hb.y, disc.y) : -1.f;
+    float t[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const float* q = sp[s];
+        const float ocx = o.x - q[0], ocy = o.y - q[1], ocz = o.z - q[2];
+        const float hb = (ocx * d.x + ocy * d.y) + ocz * d.z;
+        const float qc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - q[3];
+        const float disc = hb * hb - qa * qc;
+        t[s] = reach[s] && !(LATE && sphere_beyond(qa, hb, disc, closest)) ? sphere_root(qa, hb, disc) : -1.f;
+    }
     const int ra = __float_as_int(sa[4]), rb = __float_as_int(sb[4]);
-    if (ta >= 0.f && better(ta, ra, closest, hit)) { closest = ta; hit = ra; }
-    if (tb >= 0.f && better(tb, rb, closest, hit)) { closest = tb; hit = rb; }
+    if (t[0] >= 0.f && better(t[0], ra, closest, hit)) { closest = t[0]; hit = ra; }
+    if (t[1] >= 0.f && better(t[1], rb, closest, hit)) { closest = t[1]; hit = rb; }
 }
 
 // inv: AABB::hit's 1/d, bit-exact (recip_exact_any), shared with the traversal.
