@@ -77,6 +77,10 @@ struct RenderParams {
                                           // crit_threshold parked lanes instead of regen_threshold
 };
 
+#ifdef CRT_PROFILE_PAIRS
+__device__ unsigned long long g_pair_hist[32];   // [0, 16): log2 buckets of leaf pairs per wave step; [16, 25): lanes / 8
+#endif
+
 struct TraceCounts {
     uint32_t boxes, tris, spheres, step_slots, round_slots, trace_calls;
     // COUNT-mode section profile (variant 4; wave-uniform shader-clock cycles, s_memtime)
@@ -869,6 +873,17 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
     node_step4<COUNT>(P, o, inv, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
     const uint64_t c1 = COUNT ? shader_clock() : 0;
     if (COUNT) cnt.cyc_step += c1 - c0;
+#ifdef CRT_PROFILE_PAIRS
+    // profiling build (tools/pair_histogram.py): per wave step, the lanes stepping and the leaf pairs, log2 buckets
+    {
+        const uint32_t n_step = (uint32_t)__popcll(wave_ballot(node >= 0 || leaf_n > 0));
+        const int tot = __builtin_amdgcn_readlane(wave_inclusive_scan(leaf_n, lane), 63);
+        if (lane_fresh() == 0) {
+            atomicAdd(&g_pair_hist[tot == 0 ? 0 : 1 + min(31 - __clz(tot), 14)], 1ull);
+            atomicAdd(&g_pair_hist[16 + min(n_step >> 3, 8u)], 1ull);
+        }
+    }
+#endif
     if (!wave_ballot(leaf_n > 0)) return;
     const int incl = wave_inclusive_scan(leaf_n, lane);
     const int total = __builtin_amdgcn_readlane(incl, 63);
@@ -2946,6 +2961,18 @@ uint32_t* crt_renderer_rng_device_ptr(crt_renderer* R) { return R ? R->d_rng : n
 
 const char* crt_renderer_last_kernel_name(const crt_renderer* R) { return R ? R->kernel_name : ""; }
 
+#ifdef CRT_PROFILE_PAIRS
+extern "C" int crt_profile_pair_hist(unsigned long long* out32, int reset) {
+    if (!out32) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_pair_hist), 32 * 8, 0, hipMemcpyDeviceToHost));
+    if (reset) {
+        static const unsigned long long zero[32] = {};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pair_hist), zero, sizeof zero, 0, hipMemcpyHostToDevice));
+    }
+    return CRT_OK;
+}
+#endif
 #ifdef CRT_PROFILE_WAVE_TIMES
 extern "C" int crt_profile_wave_times(unsigned long long* out, int n_waves) {
     if (!out || n_waves <= 0 || n_waves > 4 * 65536) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
