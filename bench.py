@@ -93,6 +93,9 @@ def parse():
                     help="parked lanes before a regeneration pass (default: the library's, 44 for 4-wide scenes)")
     ap.add_argument("--occupancy", type=int, default=None,
                     help="render-kernel occupancy target in waves per SIMD (default: the library's, 6 for 4-wide scenes)")
+    ap.add_argument("--probe-spp", type=int, default=None,
+                    help="cost-probe samples per pixel before a variant-8 render (default: the library's automatic "
+                         "choice, 4 for >= 1000 spp else 2; 0 = no probe)")
     ap.add_argument("--critical-tiles", type=int, default=None,
                     help="variant 8: leading tiles of the cost order that regenerate sooner (default: library's)")
     ap.add_argument("--critical-lanes", type=int, default=16, help="their regeneration threshold")
@@ -296,6 +299,8 @@ def main():
         r.set_regen_threshold(args.regen_threshold)
     if args.occupancy is not None:
         r.set_occupancy_target(args.occupancy)
+    if args.probe_spp is not None:
+        r.set_schedule(args.probe_spp, 64)
     if args.critical_tiles is not None:
         r.set_critical_tiles(args.critical_tiles, args.critical_lanes)
     r.set_camera(cam)
