@@ -587,11 +587,17 @@ __device__ __forceinline__ float4 node_row(const float4* __restrict__ nodes, uin
 // max(t_lo, t_hi): the same box hits and tmin as the min/max form, bit for bit, without its 24 min/max per node.  The
 // row choice is an address bit (the sign of inv, shifted to the row's 16-B slot), not a select.
 __device__ __forceinline__ uint32_t sign_row(float inv) { return (__float_as_uint(inv) >> 27) & 16u; }
-__device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ nodes, uint32_t b, V3 o, V3 inv, float tmax) {
-    const uint32_t sx = sign_row(inv.x), sy = sign_row(inv.y), sz = sign_row(inv.z);
-    const float4 nxr = *rec_at(nodes, b ^ sx), fxr = *rec_at(nodes, b ^ (16u ^ sx));
-    const float4 nyr = *rec_at(nodes, b ^ (32u ^ sy)), fyr = *rec_at(nodes, b ^ (48u ^ sy));
-    const float4 nzr = *rec_at(nodes, b ^ (64u ^ sz)), fzr = *rec_at(nodes, b ^ (80u ^ sz));
+// The ray's entry-row offsets for the three axes, one byte each (row 2a ^ sign, in 16-B units), computed once per
+// ray: a node step then needs one xor per row address instead of re-deriving the signs.
+__device__ __forceinline__ uint32_t ray_rows(V3 inv) {
+    return sign_row(inv.x) | ((32u ^ sign_row(inv.y)) << 8) | ((64u ^ sign_row(inv.z)) << 16);
+}
+__device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ nodes, uint32_t b, uint32_t rows, V3 o, V3 inv,
+                                            float tmax) {
+    const uint32_t ex = b ^ (rows & 0xffu), ey = b ^ ((rows >> 8) & 0xffu), ez = b ^ (rows >> 16);
+    const float4 nxr = *rec_at(nodes, ex), fxr = *rec_at(nodes, ex ^ 16u);
+    const float4 nyr = *rec_at(nodes, ey), fyr = *rec_at(nodes, ey ^ 16u);
+    const float4 nzr = *rec_at(nodes, ez), fzr = *rec_at(nodes, ez ^ 16u);
     // one v_fma_f32 per plane: a v_pk_fma_f32 costs the SIMD the same cycles as two (MI355X_MICROARCH.md) and needs
     // {inv, inv} / {-o*inv, -o*inv} register pairs, which made the persistent variant 7 spill in this step (the
     // scalar form: variant 8 -1.7 %, variant 7 -18 %, profiles/r02aa)
@@ -729,7 +735,7 @@ __device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict
     int stack[64];
     while (node >= 0) {
         const uint32_t b = node_base(node);
-        const Wide4 w = wide_boxes(nodes, b, o, box_inv(inv), closest);
+        const Wide4 w = wide_boxes(nodes, b, ray_rows(box_inv(inv)), o, box_inv(inv), closest);
         const float4 mf = node_row(nodes, b, 6);
         const int first_child = __float_as_int(mf.x), n_int = __float_as_int(mf.y) & 0xff;
         const uint32_t counts = __float_as_uint(mf.w);
@@ -784,7 +790,7 @@ __device__ __forceinline__ int lane_fresh() {
 }
 
 template <bool COUNT>
-__device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, int& node, int& sp, float closest,
+__device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, uint32_t rows, int& node, int& sp, float closest,
                                            TraceCounts& cnt, uint32_t* __restrict__ stk, int lane, size_t pix,
                                            size_t n_pix, int& leaf_first, int& leaf_n) {
     leaf_n = 0;
@@ -792,7 +798,7 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
     if (node >= 0) {
         const uint32_t b = node_base(node);
         const float4 mf = node_row(P.nodes, b, 6);
-        const Wide4 w = wide_boxes(P.nodes, b, o, inv, closest);
+        const Wide4 w = wide_boxes(P.nodes, b, rows, o, inv, closest);
         // keep the whole link row in the node's loads: left to itself the compiler loads leaf_first / counts
         // only inside the leaf branch, one more dependent load on a leaf step's critical path.  Pinned after the
         // box tests, so the wait it implies is the one the boxes need anyway (pinned before them, it made the six
@@ -864,13 +870,13 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
 }
 
 template <bool COUNT>
-__device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d, V3 inv, int& node, int& sp,
+__device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
                                                float& closest, int& hit, TraceCounts& cnt, WaveLds& L,
                                                uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix) {
     if (COUNT) cnt.step_slots++;
     const uint64_t c0 = COUNT ? shader_clock() : 0;
     int leaf_n, leaf_first;
-    node_step4<COUNT>(P, o, inv, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
+    node_step4<COUNT>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
     const uint64_t c1 = COUNT ? shader_clock() : 0;
     if (COUNT) cnt.cyc_step += c1 - c0;
 #ifdef CRT_PROFILE_PAIRS
@@ -1174,6 +1180,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         int node = -1, sp = 0, hit = -1, px = 0, py = 0, ppix = 0;
         float closest = INF;
         V3 inv = v3(0.f, 0.f, 0.f);
+        uint32_t rows = 0;         // ray_rows(inv)
         uint32_t pool = 0, used = 64;    // wave-uniform: first slot of the reserved block, slots handed out
         bool exhausted = false;
         L.owner_at[lane] = 0;
@@ -1248,6 +1255,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     hit = -1;
                     inv = v3(recip_exact_any(S.d.x), recip_exact_any(S.d.y), recip_exact_any(S.d.z));
                     inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
+                    rows = ray_rows(inv);
                     if (COUNT) cnt.spheres += P.n_ray_spheres;
                     L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                     if (COUNT) cnt.trace_calls++;
@@ -1255,7 +1263,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 if (!wave_ballot(live)) break;      // the queue is empty and every lane is done
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
-            traverse_step4<COUNT>(P, S.o, S.d, inv, node, sp, closest, hit, cnt, L, stk, lane, (size_t)ppix, n_pix);
+            traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)ppix, n_pix);
         }
     } else if (WIDE) {
         // Same scheduling as variant 3 over a 4-wide BVH: node < 0 = no node left (lane parked).
@@ -1271,6 +1279,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         int node = -1, sp = 0, hit = -1;
         float closest = INF;
         V3 inv = v3(0.f, 0.f, 0.f);
+        uint32_t rows = 0;         // ray_rows(inv)
         L.owner_at[lane] = 0;      // traverse_step4: owner + 1, 0 = none
         // variant 8: the most expensive tiles of the cost order bound the frame when it has few tiles per wave slot
         // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
@@ -1311,6 +1320,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         // would do with rcp)
                         inv = v3(recip_exact_any(S.d.x), recip_exact_any(S.d.y), recip_exact_any(S.d.z));
                         inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
+                        rows = ray_rows(inv);
                         if (COUNT) cnt.spheres += P.n_ray_spheres;
                         L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                         if (COUNT) cnt.trace_calls++;
@@ -1321,7 +1331,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 if (TILED) wave_rays += (uint32_t)__popcll(parked_mask & live_mask);
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
-            traverse_step4<COUNT>(P, S.o, S.d, inv, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
+            traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
         }
     } else if (VARIANT == 2 || VARIANT == 3) {
         constexpr bool PF = VARIANT == 3;
