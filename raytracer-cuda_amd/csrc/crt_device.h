@@ -116,11 +116,11 @@ __device__ __forceinline__ uint32_t next_u32(Rng& s) {
 // curand_uniform: (float)x * 2^-32 + 2^-33 (CURAND_2POW32_INV and half of it).  Both constants are VOP2 literals, so
 // no register holds them (an fma form, one rounding of the same exact product, needs both in VGPRs on gfx950 and
 // measured +1.3 % through register pressure, profiles/r02t).
-__device__ __forceinline__ float uniform(Rng& s) { return (float)next_u32(s) * 0x1p-32f + 0x1p-33f; }
+__device__ __forceinline__ float uniform(Rng& s) { return __builtin_fmaf((float)next_u32(s), 0x1p-32f, 0x1p-33f); }
 // Utility.cuh:18-21: min + (max - min) * U, here min=-1, max=1: -1 + 2 * fl(X * 2^-32 + 2^-33).  (float)x has at most 24
 // significant bits, so X * 2^-32 is exact and doubling commutes with the rounding: 2 * U = fl(X * 2^-31 + 2^-32), one
 // multiply fewer than the literal restatement, the same bits.
-__device__ __forceinline__ float rand_pm1(Rng& s) { return -1.0f + ((float)next_u32(s) * 0x1p-31f + 0x1p-32f); }
+__device__ __forceinline__ float rand_pm1(Rng& s) { return __builtin_fmaf(uniform(s), 2.0f, -1.0f); }
 
 __device__ __forceinline__ V3 rand_unit_vector(Rng& s) {   // Utility.cuh:45-53, :73-76
     V3 p;

@@ -225,6 +225,26 @@ __device__ __forceinline__ int wave_inclusive_scan(int x, int /*lane*/) {
     x += __builtin_amdgcn_update_dpp(0, x, CRT_DPP_BCAST31, 0xc, 0xf, false);
     return x;
 }
+// The same scan as six in-place v_add_u32_dpp.  In traverse_step4 the combiner leaves the builtin form as v_mov_dpp +
+// v_add pairs (it reuses the partial sums for the exclusive prefix): 14 VALU instead of 6.  The s_nops are the
+// VALU-write -> DPP-read wait states, which the compiler does not insert inside an asm block.
+__device__ __forceinline__ int wave_inclusive_scan_dpp(int x) {
+    __asm__ volatile(
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+        : "+v"(x));
+    return x;
+}
 // Inclusive max-scan of non-negative values (0 = none) with the same structure.
 __device__ __forceinline__ uint32_t wave_inclusive_max_scan_u(uint32_t x) {
     x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CRT_DPP_ROW_SHR(1), 0xf, 0xf, true));
@@ -492,7 +512,7 @@ __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, 
         }
     }
     if (!wave_ballot(leaf_n > 0)) return;
-    const int incl = wave_inclusive_scan(leaf_n, lane);
+    const int incl = wave_inclusive_scan_dpp(leaf_n);
     const int total = __builtin_amdgcn_readlane(incl, 63);
     const int pfx = incl - leaf_n;
     if (leaf_n > 0) {
@@ -891,7 +911,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
     }
 #endif
     if (!wave_ballot(leaf_n > 0)) return;
-    const int incl = wave_inclusive_scan(leaf_n, lane);
+    const int incl = wave_inclusive_scan_dpp(leaf_n);
     const int total = __builtin_amdgcn_readlane(incl, 63);
     const int pfx = incl - leaf_n;
     if (leaf_n > 0) {
