@@ -78,6 +78,15 @@ __device__ __forceinline__ float recip_exact_wave(float x) {
     return 1.0f / x;
 }
 
+// a / b from r = RN(1 / b): q0 = RN(a * r), the residual a - q0 * b (exact in one FMA), one correction step (Markstein's
+// division iteration).  For next_ray's image coordinates (x + U) / width and / height only, and only for a frame size
+// whose every reachable numerator was checked against the IEEE division on the device (crt_renderer_create,
+// crt_uv_div_check_kernel); other sizes divide.
+__device__ __forceinline__ float uv_div(float a, float b, float r) {
+    const float q0 = a * r;
+    return __builtin_fmaf(__builtin_fmaf(-q0, b, a), r, q0);
+}
+
 struct V3 { float x, y, z; };
 
 __device__ __forceinline__ V3 v3(float a, float b, float c) { return V3{a, b, c}; }

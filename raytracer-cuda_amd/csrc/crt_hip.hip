@@ -61,6 +61,8 @@ struct RenderParams {
     float sph2[2][12];
     unsigned* err;                // device error flag (bit 0: primitive index out of range)
     int width, height, spp, max_bounces;
+    float rcp_w, rcp_h;           // next_ray's u = (x + U) / width by uv_div when fast_uv (crt_renderer_create)
+    int fast_uv;
     int accumulate;
     int regen_threshold;          // variant 2: parked lanes needed before a shading/regeneration pass
     uint32_t* __restrict__ rng;   // W*H*6 (v0..v4, d)
@@ -689,9 +691,10 @@ __device__ __forceinline__ void ray_spheres2(const float* sa, const float* sb, V
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         const float* q = sp[s];
-        const float t0x = (q[5] - o.x) * inv.x, t1x = (q[8] - o.x) * inv.x;
-        const float t0y = (q[6] - o.y) * inv.y, t1y = (q[9] - o.y) * inv.y;
-        const float t0z = (q[7] - o.z) * inv.z, t1z = (q[10] - o.z) * inv.z;
+        const float4 lo = *reinterpret_cast<const float4*>(q + 4), hi = *reinterpret_cast<const float4*>(q + 8);
+        const float t0x = (lo.x - o.x) * inv.x, t1x = (lo.w - o.x) * inv.x;
+        const float t0y = (lo.y - o.y) * inv.y, t1y = (hi.x - o.y) * inv.y;
+        const float t0z = (lo.z - o.z) * inv.z, t1z = (hi.y - o.z) * inv.z;
         float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
         float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
         tmin = fmaxf(tmin, 0.001f);
@@ -702,14 +705,14 @@ __device__ __forceinline__ void ray_spheres2(const float* sa, const float* sb, V
     float t[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-        const float* q = sp[s];
-        const float ocx = o.x - q[0], ocy = o.y - q[1], ocz = o.z - q[2];
+        const float4 c = *reinterpret_cast<const float4*>(sp[s]);
+        const float ocx = o.x - c.x, ocy = o.y - c.y, ocz = o.z - c.z;
         const float hb = (ocx * d.x + ocy * d.y) + ocz * d.z;
-        const float qc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - q[3];
+        const float qc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - c.w;
         const float disc = hb * hb - qa * qc;
         t[s] = reach[s] && !(LATE && sphere_beyond(qa, hb, disc, closest)) ? sphere_root(qa, hb, disc) : -1.f;
     }
-    const int ra = __float_as_int(sa[4]), rb = __float_as_int(sb[4]);
+    const int ra = __float_as_int(sa[10]), rb = __float_as_int(sb[10]);
     if (t[0] >= 0.f && better(t[0], ra, closest, hit)) { closest = t[0]; hit = ra; }
     if (t[1] >= 0.f && better(t[1], rb, closest, hit)) { closest = t[1]; hit = rb; }
 }
@@ -721,7 +724,7 @@ __device__ __forceinline__ void ray_spheres(const float4* __restrict__ prims, co
                                             int& hit, const float* sph2 = nullptr) {
     if (n == 0) return;
     if (n == 2 && sph2) {
-        ray_spheres2<LATE>(sph2, sph2 + 12, o, d, inv, closest, hit);
+        ray_spheres2<LATE>(sph2, sph2 + 16, o, d, inv, closest, hit);
         return;
     }
     for (int s = 0; s < n; ++s) {
@@ -973,6 +976,8 @@ struct PathState {
 struct CamRegs {
     V3 pos, llc, hor, ver, right, up;
     float lens, fw, fh;
+    float rfw, rfh;   // RN(1 / fw), RN(1 / fh) (host IEEE division)
+    int fast_uv;      // uv_div is verified exact for this frame size (crt_renderer_create): no IEEE division
 };
 
 // Phase 1: give the lane a ray to trace — Camera::getRay for a new sample, the bounce-limit exit and
@@ -992,8 +997,17 @@ __device__ __forceinline__ bool next_ray(PathState& S, const CamRegs& C, int x, 
             const V3 rd = C.lens * v3(da, db, 0);
             const V3 off = v3(C.right.x * rd.x, C.right.y * rd.x, C.right.z * rd.x) +
                            v3(C.up.x * rd.y, C.up.y * rd.y, C.up.z * rd.y);
-            const float u = ((float)x + uniform(S.s)) / C.fw;
-            const float v = ((float)y + uniform(S.s)) / C.fh;
+            const float au = (float)x + uniform(S.s);
+            const float av = (float)y + uniform(S.s);
+            float u, v;
+            if (C.fast_uv) {
+                u = uv_div(au, C.fw, C.rfw);
+                v = uv_div(av, C.fh, C.rfh);
+            } else {
+                __asm__ volatile("");   // a real branch: no if-conversion that would run both divisions
+                u = au / C.fw;
+                v = av / C.fh;
+            }
             S.o = C.pos + off;
             S.d = (((C.llc + u * C.hor) + v * C.ver) - C.pos) - off;
             S.thr = v3(1.0f, 1.0f, 1.0f);
@@ -1034,6 +1048,9 @@ __device__ __forceinline__ bool cannot_refract_exact(float cos_theta, float ri) 
     const double z = (r * r) * y;
     const bool above = z > 1.0 + 0x1p-40, below = z < 1.0 - 0x1p-40;
     if (__builtin_amdgcn_ballot_w64(!(above || below)) == 0) return above;
+    // keeps the f64 sqrt behind the branch: without it the compiler if-converts the uniform branch and computes the
+    // sqrt sequence in every wave with a glass hit, then selects
+    __asm__ volatile("");
     return r * sqrt(y) > 1.0;
 }
 
@@ -1131,9 +1148,15 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     constexpr bool WIDE = VARIANT == 4 || PERSIST || TILED;
     constexpr int SD = WIDE ? (MINW >= 7 ? 11 : MINW >= 6 ? 12 : STACK_LDS) : 1;
     __shared__ uint32_t stack_lds[WIDE ? WGW * SD * 64 : 1];
-    __shared__ float sph_lds[24];
+    // the two per-ray spheres in 16-B rows, so every read is one ds_read_b128 at a fixed offset: per sphere
+    // (center.xyz, radius^2) (box lo.xyz, box hi.x) (box hi.yz, rank, 0) (unused)
+    __shared__ __attribute__((aligned(16))) float sph_lds[32];
     if (WIDE) {
-        if (threadIdx.x < 24) sph_lds[threadIdx.x] = (&P.sph2[0][0])[threadIdx.x];
+        if (threadIdx.x < 32) {
+            const int k = threadIdx.x & 15;
+            const int src = k < 4 ? k : k < 9 ? k + 1 : k == 9 ? 10 : k == 10 ? 4 : -1;
+            sph_lds[threadIdx.x] = src < 0 ? 0.f : P.sph2[threadIdx.x >> 4][src];
+        }
         __syncthreads();
     }
     // 16x16 pixel tile per workgroup, 8x8 per wave64.
@@ -1173,6 +1196,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     C.lens = Cd.lens_radius;
     C.fw = (float)P.width;
     C.fh = (float)P.height;
+    C.rfw = P.rcp_w;
+    C.rfh = P.rcp_h;
+    C.fast_uv = P.fast_uv;
     TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t wave_rays = 0;    // variant 8: rays of the wave (uniform); the other variants count per lane
 
@@ -1497,6 +1523,9 @@ __global__ __launch_bounds__(256) void crt_compare_kernel(CompareParams Q) {
     C.lens = Cd.lens_radius;
     C.fw = (float)P.width;
     C.fh = (float)P.height;
+    C.rfw = P.rcp_w;
+    C.rfh = P.rcp_h;
+    C.fast_uv = P.fast_uv;
     TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long n_rank = 0, n_t = 0, n_bmiss = 0, n_amiss = 0;
     while (next_ray(S, C, x, y, P.max_bounces)) {
@@ -1616,6 +1645,20 @@ __global__ __launch_bounds__(256) void crt_selftest_rcp_kernel(uint32_t lo, uint
     if (nbad) atomicAdd(bad, nbad);
 }
 
+// Exhaustive check of next_ray's division for one frame dimension b: every float a in [lo, hi] (all values (x + U) can
+// take) through uv_div against IEEE a / b.
+__global__ __launch_bounds__(256) void crt_uv_div_check_kernel(float b, float r, uint32_t lo, uint32_t hi,
+                                                               unsigned long long* bad) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    unsigned long long nbad = 0;
+    for (uint32_t i = lo + blockIdx.x * blockDim.x + threadIdx.x; i <= hi && i >= lo; i += stride) {
+        const float a = __uint_as_float(i);
+        if (__float_as_uint(uv_div(a, b, r)) != __float_as_uint(a / b)) ++nbad;
+        if (i > 0xffffffffu - stride) break;
+    }
+    if (nbad) atomicAdd(bad, nbad);
+}
+
 __global__ __launch_bounds__(64) void crt_selftest_scan_kernel(const int* in, int* out, int n_waves) {
     const int w = blockIdx.x;
     if (w >= n_waves) return;
@@ -1632,7 +1675,8 @@ __global__ __launch_bounds__(64) void crt_selftest_scan_kernel(const int* in, in
 // [0.001, inf) with the exact 1/d), 2 = sphere_candidate (Sphere::hit, window [0.001, tmax]), 3 = next_ray's
 // Camera::getRay for a new sample.
 __global__ void crt_selftest_geometry_kernel(int kind, const float* __restrict__ in, int n, float* __restrict__ out,
-                                             uint32_t* __restrict__ rng, crt_camera_desc cam, int w, int h) {
+                                             uint32_t* __restrict__ rng, crt_camera_desc cam, int w, int h, float rcp_w,
+                                             float rcp_h, int fast_uv) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     if (kind == 0) {
@@ -1672,6 +1716,9 @@ __global__ void crt_selftest_geometry_kernel(int kind, const float* __restrict__
         C.lens = cam.lens_radius;
         C.fw = (float)w;
         C.fh = (float)h;
+        C.rfw = rcp_w;
+        C.rfh = rcp_h;
+        C.fast_uv = fast_uv;
         PathState S;
         uint32_t* r = rng + 6 * (size_t)i;
         S.s = Rng{r[0], r[1], r[2], r[3], r[4], r[5]};
@@ -2254,6 +2301,8 @@ struct crt_renderer {
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
     size_t ovf_entries = 0;
     int stack_lds = STACK_LDS;     // variant 4: per-lane stack entries kept in LDS
+    float rcp_w = 1.f, rcp_h = 1.f; // RN(1 / width), RN(1 / height)
+    int fast_uv = 0;               // next_ray divides by uv_div (verified for this size at creation, uv_div_mismatches)
     // variant 5 (wavefront) state, allocated on first use
 };
 
@@ -2501,6 +2550,34 @@ void crt_scene_destroy(crt_scene* S) {
     delete S;
 }
 
+namespace {
+// Mismatches of uv_div(a, b, RN(1 / b)) against a / b over every a next_ray can form for an image dimension b:
+// a = fl(x + U) with x in [0, b - 1] and U = fl(X * 2^-32 + 2^-33) in [2^-33, 1], so a in [2^-33, b].
+constexpr uint32_t UV_A_MIN_BITS = 0x2f000000u;   // 2^-33
+int uv_div_mismatches(int dim, unsigned long long* out) {
+    const float b = (float)dim, r = 1.0f / b;
+    uint32_t hi;
+    std::memcpy(&hi, &b, 4);
+    unsigned long long* d;
+    HIP_TRY(hipMalloc((void**)&d, 8));
+    hipError_t e = hipMemset(d, 0, 8);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(crt_uv_div_check_kernel, dim3(4096), dim3(256), 0, 0, b, r, UV_A_MIN_BITS, hi, d);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, d, 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    HIP_TRY(e);
+    return CRT_OK;
+}
+}  // namespace
+
+int crt_selftest_uv_div(int dim, unsigned long long* mismatches) {
+    if (dim <= 0 || !mismatches) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    if (int rc = use_device(0)) return rc;
+    return uv_div_mismatches(dim, mismatches);
+}
+
 int crt_renderer_create(int width, int height, int device, crt_renderer** out) {
     if (!out || width <= 0 || height <= 0 || (long long)width * height > (1LL << 31) / 6)
         return set_error(CRT_ERR_INVALID_ARGUMENT, "bad renderer size");
@@ -2527,6 +2604,17 @@ int crt_renderer_create(int width, int height, int device, crt_renderer** out) {
                          std::string("renderer allocation: ") + hipGetErrorString(e));
     }
     R->d_sum = R->d_sum_own;
+    // next_ray's image-coordinate divisions: uv_div when it equals the IEEE division for every input of this size
+    unsigned long long bad_w = 0, bad_h = 0;
+    int rc = uv_div_mismatches(width, &bad_w);
+    if (rc == CRT_OK) rc = height == width ? CRT_OK : uv_div_mismatches(height, &bad_h);
+    if (rc != CRT_OK) {
+        crt_renderer_destroy(R);
+        return rc;
+    }
+    R->rcp_w = 1.0f / (float)width;
+    R->rcp_h = 1.0f / (float)height;
+    R->fast_uv = bad_w == 0 && bad_h == 0;
     *out = R;
     return CRT_OK;
 }
@@ -2667,6 +2755,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
     P.accumulate = (flags & CRT_RENDER_ACCUMULATE) ? 1 : 0;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
+    P.rcp_w = R->rcp_w; P.rcp_h = R->rcp_h; P.fast_uv = R->fast_uv;
     P.ovf = nullptr;
     P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0; P.crit_tiles = 0; P.crit_threshold = 64;
     P.stack_cap = S->stack_cap;
@@ -2867,6 +2956,7 @@ int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene*
     P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
     P.accumulate = 0; P.regen_threshold = 64;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
+    P.rcp_w = R->rcp_w; P.rcp_h = R->rcp_h; P.fast_uv = R->fast_uv;
     Q.nodes_b = B->d_nodes; Q.prims_b = B->d_prims; Q.n_nodes_b = B->n_nodes; Q.n_layouts_b = B->layouts;
     Q.width_a = A->width; Q.width_b = B->width;
     Q.dump = nullptr;
@@ -3086,9 +3176,15 @@ int crt_selftest_geometry(int kind, const float* in, int n, const crt_camera_des
     hipError_t e = hipMemcpy(din, in, (size_t)n * in_words[kind] * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess && kind == 3) e = hipMemcpy(drng, rng, (size_t)n * 24, hipMemcpyHostToDevice);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(crt_selftest_geometry_kernel, dim3((n + 63) / 64), dim3(64), 0, 0, kind, din, n, dout, drng,
-                           cam ? *cam : crt_camera_desc{}, width, height);
-        e = hipGetLastError();
+        unsigned long long bad_w = 0, bad_h = 0;   // the renderer's choice for this size (crt_renderer_create)
+        if (kind == 3 && (uv_div_mismatches(width, &bad_w) != CRT_OK || uv_div_mismatches(height, &bad_h) != CRT_OK))
+            e = hipErrorUnknown;
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(crt_selftest_geometry_kernel, dim3((n + 63) / 64), dim3(64), 0, 0, kind, din, n, dout,
+                               drng, cam ? *cam : crt_camera_desc{}, width, height, kind == 3 ? 1.0f / (float)width : 1.f,
+                               kind == 3 ? 1.0f / (float)height : 1.f, (int)(kind == 3 && bad_w == 0 && bad_h == 0));
+            e = hipGetLastError();
+        }
     }
     if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * out_words[kind] * 4, hipMemcpyDeviceToHost);
     if (e == hipSuccess && kind == 3) e = hipMemcpy(rng, drng, (size_t)n * 24, hipMemcpyDeviceToHost);

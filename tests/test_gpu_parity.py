@@ -68,6 +68,23 @@ def test_fast_reciprocal_exhaustive():
     assert bad.value == 0, f"{bad.value} mismatches, first bits {first.value:#010x}"
 
 
+# frame dimensions of the configs (A 256x256, B 1280x720, C/E 2560x1440), the parity crops and the viewer, plus a
+# spread of others (odd, prime, 2^k - 1, 4K)
+UV_DIMS = [1, 2, 3, 7, 64, 72, 96, 128, 160, 256, 640, 720, 1000, 1023, 1080, 1280, 1440, 1919, 2160, 2560, 3840, 4093]
+
+
+def test_uv_division_exhaustive():
+    """uv_div(a, dim, RN(1/dim)) == IEEE a / dim for every float a in [2^-33, dim], i.e. every (x + U) next_ray can form
+    (crt_device.h::uv_div).  crt_renderer_create runs the same check and divides when it fails; at these sizes it
+    never does, so the frames of every parity test run the fast path."""
+    import ctypes as C
+    from crt_amd import _lib
+    for dim in UV_DIMS:
+        bad = C.c_ulonglong(0)
+        crt_amd.check(_lib.hip().crt_selftest_uv_div(dim, C.byref(bad)))
+        assert bad.value == 0, f"dim {dim}: {bad.value} mismatches"
+
+
 def test_wave_scans():
     import ctypes as C
     from crt_amd import _lib
