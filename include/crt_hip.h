@@ -306,6 +306,10 @@ int crt_selftest_math(const float* a, const float* b, int n, float* out, double*
 /* Exhaustive reciprocal self-test: counts floats x with bit patterns in [lo_bits, hi_bits) (and -x) for which
  * the kernel's fast reciprocal (v_rcp_f32 + FMA Newton step) differs from IEEE 1.f/x; first_bad = lowest such. */
 int crt_selftest_rcp(uint32_t lo_bits, uint32_t hi_bits, unsigned long long* mismatches, uint32_t* first_bad);
+/* Exhaustive square-root self-test: counts floats x with bit patterns in [lo_bits, hi_bits) for which the kernels'
+ * fast square root (v_rsq_f32 + one FMA correction step, crt_device.h::sqrt_rsq) differs from the correctly rounded
+ * sqrtf; first_bad = lowest such. */
+int crt_selftest_sqrt(uint32_t lo_bits, uint32_t hi_bits, unsigned long long* mismatches, uint32_t* first_bad);
 /* Exhaustive check of next_ray's image-coordinate division for one frame dimension (width or height): counts the
  * floats a in [2^-33, dim] (every value x + U can take) for which uv_div(a, dim, RN(1/dim)) differs from IEEE a / dim.
  * crt_renderer_create runs the same check and uses uv_div only when both dimensions have none. */

@@ -103,7 +103,7 @@ HIP_SYMBOLS = [
     "crt_renderer_set_regen_threshold", "crt_renderer_set_occupancy_target",
     "crt_build_mesh_bvh", "crt_renderer_set_schedule", "crt_renderer_set_critical_tiles",
     "crt_selftest_math", "crt_selftest_rng", "crt_selftest_geometry", "crt_selftest_scan", "crt_selftest_rcp",
-    "crt_selftest_uv_div",
+    "crt_selftest_uv_div", "crt_selftest_sqrt",
 ]
 HOST_SYMBOLS = [
     "crth_scene_load", "crth_scene_load_ex", "crth_scene_build_ms", "crth_scene_destroy", "crth_scene_desc", "crth_scene_upload", "crth_scene_upload_ex", "crth_scene_counts",
@@ -175,6 +175,7 @@ def hip():
             "crt_selftest_scan": ([P, i32, P], i32),
             "crt_selftest_rcp": ([C.c_uint32, C.c_uint32, P, P], i32),
             "crt_selftest_uv_div": ([i32, P], i32),
+            "crt_selftest_sqrt": ([C.c_uint32, C.c_uint32, P, P], i32),
         }
         for name, (args, res) in sig.items():
             if os.environ.get("CRT_HIP_LIB") and not hasattr(L, name):

@@ -87,6 +87,25 @@ __device__ __forceinline__ float uv_div(float a, float b, float r) {
     return __builtin_fmaf(__builtin_fmaf(-q0, b, a), r, q0);
 }
 
+// sqrtf(x) bit for bit: r = v_rsq_f32(x), s0 = x * r, one correction step s0 + (x - s0 * s0) * (r / 2) (the residual
+// exact in one FMA).  Exhaustively verified on gfx950 against the correctly rounded sqrtf for EVERY float in
+// [2^-100, FLT_MAX] (tools/probes/sqrt_probe.hip, profiles/r02an; crt_selftest_sqrt, tests/test_gpu_parity.py).
+// 5 VALU instead of the ~16 of the compiler's correctly rounded sequence (raw v_sqrt_f32 is off by one ulp for ~16 %
+// of inputs, profiles/r01k).
+constexpr float SQRT_FAST_MIN = 0x1p-100f;
+__device__ __forceinline__ float sqrt_rsq(float x) {
+    const float r = __builtin_amdgcn_rsqf(x);
+    const float s0 = x * r;
+    return __builtin_fmaf(__builtin_fmaf(-s0, s0, x), 0.5f * r, s0);
+}
+// sqrtf(x) for ANY x: sqrt_rsq when every active lane's x lies in the verified range (a wave-uniform branch), else the
+// IEEE sequence (0, denormals, x < 2^-100, inf, NaN, negative).
+__device__ __forceinline__ float sqrt_exact_wave(float x) {
+    if (__builtin_amdgcn_ballot_w64(!(x >= SQRT_FAST_MIN && x <= 3.40282347e38f)) == 0) return sqrt_rsq(x);
+    __asm__ volatile("");   // keeps the branch: no if-conversion that would run both sequences
+    return sqrtf(x);
+}
+
 struct V3 { float x, y, z; };
 
 __device__ __forceinline__ V3 v3(float a, float b, float c) { return V3{a, b, c}; }
@@ -100,13 +119,14 @@ __device__ __forceinline__ V3 cross(V3 u, V3 v) {                               
     return v3(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
 }
 __device__ __forceinline__ float len2(V3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }            // :95
-// Vec3::unit: (1 / length) * v, the reciprocal exact (recip_exact_wave; -0.5 %, profiles/r02s)
-__device__ __forceinline__ V3 unit(V3 v) { return recip_exact_wave(sqrtf(len2(v))) * v; }             // :201,:213
+// Vec3::unit: (1 / length) * v, the reciprocal and the square root exact (recip_exact_wave, -0.5 %, profiles/r02s;
+// sqrt_exact_wave, profiles/r02an)
+__device__ __forceinline__ V3 unit(V3 v) { return recip_exact_wave(sqrt_exact_wave(len2(v))) * v; }   // :201,:213
 __device__ __forceinline__ V3 reflect(V3 v, V3 n) { return v - (2.0f * dot(v, n)) * n; }              // :225
 __device__ __forceinline__ V3 refract(V3 uv, V3 n, float eta) {                                        // :229
     float cos_theta = fminf(dot(-uv, n), 1.0f);
     V3 perp = eta * (uv + cos_theta * n);
-    V3 par = (-sqrtf(fabsf(1.0f - len2(perp)))) * n;
+    V3 par = (-sqrt_exact_wave(fabsf(1.0f - len2(perp)))) * n;
     return perp + par;
 }
 

@@ -154,7 +154,7 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
                 const float qc = dot(oc, oc) - f1.x;
                 const float disc = hb * hb - qa * qc;
                 if (!(disc < 0)) {
-                    const float sq = sqrtf(disc);
+                    const float sq = sqrt_exact_wave(disc);
                     float root = (-hb - sq) / qa;
                     bool ok = true;
                     if (root < 0.001f || root > closest) {
@@ -312,7 +312,7 @@ __device__ __forceinline__ float sphere_candidate(float4 f0, float4 f1, V3 o, V3
     const float qc = dot(oc, oc) - f1.x;
     const float disc = hb * hb - qa * qc;
     if (disc < 0) return -1.f;
-    const float sq = sqrtf(disc);
+    const float sq = sqrt_exact_wave(disc);
     float root = (-hb - sq) / qa;
     if (root < 0.001f || root > tmax) {
         root = (-hb + sq) / qa;
@@ -354,7 +354,7 @@ __device__ __forceinline__ void sphere_test(const float4* __restrict__ prims, in
     const float qc = dot(oc, oc) - f1.x;
     const float disc = hb * hb - qa * qc;
     if (disc < 0) return;
-    const float sq = sqrtf(disc);
+    const float sq = sqrt_exact_wave(disc);
     float root = (-hb - sq) / qa;
     if (root < 0.001f || root > closest) {
         root = (-hb + sq) / qa;
@@ -657,7 +657,7 @@ __device__ __forceinline__ bool ref_scene_box(float4 A, float4 B, V3 o, V3 inv) 
 // Sphere::hit's candidate root from its discriminant terms (Sphere.cuh:27-47 with closest = inf).
 __device__ __forceinline__ float sphere_root(float qa, float hb, float disc) {
     if (disc < 0) return -1.f;
-    const float sq = sqrtf(disc);
+    const float sq = sqrt_exact_wave(disc);
     float root = (-hb - sq) / qa;
     if (root < 0.001f) {
         root = (-hb + sq) / qa;
@@ -1637,6 +1637,21 @@ __global__ __launch_bounds__(256) void crt_selftest_rcp_kernel(uint32_t lo, uint
         const float a = rcp_newton(x), c = 1.0f / x;
         const float an = rcp_newton(-x), cn = 1.0f / -x;
         if (__float_as_uint(a) != __float_as_uint(c) || __float_as_uint(an) != __float_as_uint(cn)) {
+            ++nbad;
+            atomicMin(first_bad, b);
+        }
+        if (b > 0xffffffffu - stride) break;
+    }
+    if (nbad) atomicAdd(bad, nbad);
+}
+
+__global__ __launch_bounds__(256) void crt_selftest_sqrt_kernel(uint32_t lo, uint32_t hi, unsigned long long* bad,
+                                                                uint32_t* first_bad) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    unsigned long long nbad = 0;
+    for (uint32_t b = lo + blockIdx.x * blockDim.x + threadIdx.x; b < hi && b >= lo; b += stride) {
+        const float x = __uint_as_float(b);
+        if (__float_as_uint(sqrt_rsq(x)) != __float_as_uint(sqrtf(x))) {
             ++nbad;
             atomicMin(first_bad, b);
         }
@@ -3139,6 +3154,24 @@ int crt_selftest_rcp(uint32_t lo_bits, uint32_t hi_bits, unsigned long long* mis
     HIP_TRY(hipMemset(dbad, 0, 8));
     HIP_TRY(hipMemset(dfirst, 0xff, 4));
     hipLaunchKernelGGL(crt_selftest_rcp_kernel, dim3(8192), dim3(256), 0, 0, lo_bits, hi_bits, dbad, dfirst);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(mismatches, dbad, 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(first_bad, dfirst, 4, hipMemcpyDeviceToHost));
+    (void)hipFree(dbad);
+    (void)hipFree(dfirst);
+    return CRT_OK;
+}
+
+int crt_selftest_sqrt(uint32_t lo_bits, uint32_t hi_bits, unsigned long long* mismatches, uint32_t* first_bad) {
+    if (!mismatches || !first_bad) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    if (int rc = use_device(0)) return rc;
+    unsigned long long* dbad;
+    uint32_t* dfirst;
+    HIP_TRY(hipMalloc((void**)&dbad, 8));
+    HIP_TRY(hipMalloc((void**)&dfirst, 4));
+    HIP_TRY(hipMemset(dbad, 0, 8));
+    HIP_TRY(hipMemset(dfirst, 0xff, 4));
+    hipLaunchKernelGGL(crt_selftest_sqrt_kernel, dim3(8192), dim3(256), 0, 0, lo_bits, hi_bits, dbad, dfirst);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpy(mismatches, dbad, 8, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(first_bad, dfirst, 4, hipMemcpyDeviceToHost));

@@ -68,6 +68,18 @@ def test_fast_reciprocal_exhaustive():
     assert bad.value == 0, f"{bad.value} mismatches, first bits {first.value:#010x}"
 
 
+def test_fast_sqrt_exhaustive():
+    """sqrt_rsq(x) == the correctly rounded sqrtf(x) for EVERY float in [2^-100, FLT_MAX]; the kernels use it only
+    when every lane of the wave is in that range (crt_device.h::sqrt_exact_wave)."""
+    import ctypes as C
+    from crt_amd import _lib
+    lo = int(np.float32(2.0 ** -100).view(np.uint32))
+    hi = 0x7f800000   # exclusive: up to FLT_MAX
+    bad, first = C.c_ulonglong(0), C.c_uint32(0)
+    crt_amd.check(_lib.hip().crt_selftest_sqrt(lo, hi, C.byref(bad), C.byref(first)))
+    assert bad.value == 0, f"{bad.value} mismatches, first bits {first.value:#010x}"
+
+
 # frame dimensions of the configs (A 256x256, B 1280x720, C/E 2560x1440), the parity crops and the viewer, plus a
 # spread of others (odd, prime, 2^k - 1, 4K)
 UV_DIMS = [1, 2, 3, 7, 64, 72, 96, 128, 160, 256, 640, 720, 1000, 1023, 1080, 1280, 1440, 1919, 2160, 2560, 3840, 4093]
