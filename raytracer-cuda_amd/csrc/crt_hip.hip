@@ -296,6 +296,31 @@ __device__ __forceinline__ float tri_test_rec(float4 f0, float4 f1, float4 f2, V
     if (t < 0.001f || t > tmax) return -1.f;
     return t;
 }
+// The same test without early exits, for the leaf rounds: u, v and t are pure functions of the record and the ray, so
+// computing them on every lane and rejecting once returns the same value (the reject predicate keeps the reference's
+// comparisons, NaN included).  1/det by rcp_newton when every active lane's |det| is below 2^126 (a wave-uniform
+// choice; lanes with |det| < 1e-8 are rejected whatever f is), else by IEEE division.
+__device__ __forceinline__ float tri_test_flat(float4 f0, float4 f1, float4 f2, V3 o, V3 d, float tmax) {
+    const V3 e1 = v3(f0.w, f1.x, f1.y);
+    const V3 e2 = v3(f1.z, f1.w, f2.x);
+    const V3 h = cross(d, e2);
+    const float det = dot(e1, h);
+    const float a = fabsf(det);
+    float f;
+    if (__builtin_amdgcn_ballot_w64(!(a < RCP_FAST_MAX)) == 0) {
+        f = rcp_newton(det);
+    } else {
+        __asm__ volatile("");
+        f = 1.0f / det;
+    }
+    const V3 s = o - v3(f0.x, f0.y, f0.z);
+    const float u = f * dot(s, h);
+    const V3 q = cross(s, e1);
+    const float v = f * dot(d, q);
+    const float t = f * dot(e2, q);
+    const bool rej = (a < 1e-8f) | (u < 0.f) | (u > 1.f) | (v < 0.f) | ((u + v) > 1.f) | (t < 0.001f) | (t > tmax);
+    return rej ? -1.f : t;
+}
 __device__ __forceinline__ float tri_test(const float4* __restrict__ prims, int p, V3 o, V3 d, float tmax, int& rank) {
     const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1], f2 = prims[3 * p + 2];
     rank = __float_as_int(f2.z);
@@ -341,7 +366,8 @@ __device__ __forceinline__ float prim_test(const float4* __restrict__ prims, int
     __asm__ volatile("" : : "v"(f2.y));
     rank = __float_as_int(f2.z);
     if (tree_spheres && __float_as_int(f2.w) == 1) return sphere_candidate(f0, f1, o, d, tmax);
-    return tri_test_rec(f0, f1, f2, o, d, tmax);
+    // without early exits: the leaf rounds are full of lanes, so the exits only cost branches (-0.75 %, profiles/r02ap)
+    return tri_test_flat(f0, f1, f2, o, d, tmax);
 }
 
 // Sphere::hit (Sphere.cuh:27-47) against [0.001, closest]; updates closest/hit (= rank) on acceptance.
@@ -874,7 +900,9 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
         };
         if (k[0] != ~0u) {
             node = first_child + (int)(k[0] & 3);
-            const uint32_t n_rest = (k[1] != ~0u) + (k[2] != ~0u) + (k[3] != ~0u);
+            // the hit internal children but the nearest (k[s] != ~0u exactly for the hit slots below n_int), as one
+            // popcount (-1.0 %, profiles/r02ap)
+            const uint32_t n_rest = (uint32_t)__popc(hm & ((1u << n_int) - 1u)) - 1u;
             if (n_rest && store(sp, ((uint32_t)first_child << 8) | (n_rest << 6) | ((k[1] & 3) << 4) |
                                         ((k[2] & 3) << 2) | (k[3] & 3)))
                 ++sp;
@@ -917,9 +945,10 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
     const int incl = wave_inclusive_scan_dpp(leaf_n);
     const int total = __builtin_amdgcn_readlane(incl, 63);
     const int pfx = incl - leaf_n;
-    if (leaf_n > 0) {
-        L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first));
-        L.prefix[lane] = pfx;
+    {   // every lane writes its own slots, only the owners' are read: no branch (-0.8 %, profiles/r02ar)
+        // leaf_first - prefix: a pair's primitive is ray1.w + its index j (-0.27 %, profiles/r02aq; round 1 measured
+        // this +2.2 %, profiles/r01aj, before the round-2 changes to the round's code)
+        L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first - pfx));
         // the empty key, materialised here: as a plain constant the register allocator keeps ~0ull live across
         // the loop and spills it (a scratch reload and a vmcnt(0) wait on every leaf step)
         uint32_t ones;
@@ -938,25 +967,24 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         const int j = base + lane;
         if (j < total) {
             const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
-            // the prefix address from its own base: derived from ray1's, the compiler builds it with a 64-bit multiply
-            int owner_p = owner;
-            __asm__("" : "+v"(owner_p));
-            const int p = __float_as_int(r1.w) + (j - L.prefix[owner_p]);   // inside the owner's checked span
+            const int p = __float_as_int(r1.w) + j;   // leaf_first - prefix + j: inside the owner's checked span
             if (COUNT) cnt.tris++;
             int rank;
             const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
                                       P.tree_spheres != 0);
-            if (t >= 0.f)
-                atomicMin(&L.key[owner], ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank));
+            // a rejected pair offers the empty key (no effect on the min): one LDS atomic per pair, no branch
+            // (-0.75 %, profiles/r02ar)
+            const unsigned long long kp = ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank);
+            atomicMin(&L.key[owner], t >= 0.f ? kp : ~0ull);
         }
         carry = __builtin_amdgcn_readlane(owner1, 63);
         wave_sync();
     }
-    if (leaf_n > 0) {
+    {
         const unsigned long long kk = L.key[lane];
         const float t = __uint_as_float((unsigned)(kk >> 32));
         const int rank = (int)(0xffffffffu - (unsigned)kk);
-        if (kk != ~0ull && better(t, rank, closest, hit)) {
+        if (leaf_n > 0 && kk != ~0ull && better(t, rank, closest, hit)) {
             closest = t;
             hit = rank;
         }
