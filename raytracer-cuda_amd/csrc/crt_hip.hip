@@ -614,6 +614,16 @@ __device__ __forceinline__ V3 box_inv(V3 inv) {
               __builtin_amdgcn_fmed3f(inv.y, -BOX_INV_CLAMP, BOX_INV_CLAMP),
               __builtin_amdgcn_fmed3f(inv.z, -BOX_INV_CLAMP, BOX_INV_CLAMP));
 }
+// 1/d of a new ray, each component == 1.f / x bit for bit: rcp_newton when every active lane's three components lie in
+// its verified range (a wave-uniform branch), else recip_exact_any per component (-0.33 %, profiles/r02av).
+__device__ __forceinline__ V3 recip3_exact(V3 d) {
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    const bool ok = ax >= RCP_FAST_MIN && ax < RCP_FAST_MAX && ay >= RCP_FAST_MIN && ay < RCP_FAST_MAX &&
+                    az >= RCP_FAST_MIN && az < RCP_FAST_MAX;
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) return v3(rcp_newton(d.x), rcp_newton(d.y), rcp_newton(d.z));
+    __asm__ volatile("");
+    return v3(recip_exact_any(d.x), recip_exact_any(d.y), recip_exact_any(d.z));
+}
 // The per-ray spheres' exact 1/d (their reference box test) from the traversal's box_inv: recomputed only when a
 // component was clamped.
 __device__ __forceinline__ V3 sphere_inv(V3 d, V3 binv) {
@@ -1327,7 +1337,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     sp = 0;
                     closest = INF;
                     hit = -1;
-                    inv = v3(recip_exact_any(S.d.x), recip_exact_any(S.d.y), recip_exact_any(S.d.z));
+                    inv = recip3_exact(S.d);
                     inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
                     rows = ray_rows(inv);
                     if (COUNT) cnt.spheres += P.n_ray_spheres;
@@ -1358,6 +1368,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         // variant 8: the most expensive tiles of the cost order bound the frame when it has few tiles per wave slot
         // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
         const int regen_t = (TILED && (int)blockIdx.x < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
+        bool first_pass = true;    // uniform
         for (;;) {
             const uint64_t parked_mask = live_mask & wave_ballot(node < 0);
             const int n_parked = __popcll(parked_mask);
@@ -1370,11 +1381,15 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     const uint64_t s0 = COUNT ? shader_clock() : 0;
                     // (loading the shading record before this sphere test, to overlap its latency, measured +0.7 %:
                     // profiles/r01ar)
-                    if (has_result)
-                        ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
-                                          sphere_inv(S.d, inv), closest, hit, sph_lds);
-                    if (COUNT) cnt.cyc_sph += shader_clock() - s0;
-                    if (has_result) shade(S, P, hit, closest);
+                    // after the first pass every parked lane holds a result (parked_mask is within live_mask, which is
+                    // the lanes with a ray): a uniform test instead of a divergent branch on has_result (-0.38 %,
+                    // profiles/r02av)
+                    if (!first_pass) {
+                        ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o,
+                                          S.d, sphere_inv(S.d, inv), closest, hit, sph_lds);
+                        if (COUNT) cnt.cyc_sph += shader_clock() - s0;
+                        shade(S, P, hit, closest);
+                    }
                     const uint64_t s1 = COUNT ? shader_clock() : 0;
                     const bool live = next_ray(S, C, x, y, P.max_bounces);
                     if (COUNT) {
@@ -1392,7 +1407,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         hit = -1;
                         // exact 1/d: the per-ray spheres' reference box tests need it (the padded traversal
                         // would do with rcp)
-                        inv = v3(recip_exact_any(S.d.x), recip_exact_any(S.d.y), recip_exact_any(S.d.z));
+                        inv = recip3_exact(S.d);
                         inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
                         rows = ray_rows(inv);
                         if (COUNT) cnt.spheres += P.n_ray_spheres;
@@ -1401,6 +1416,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     }
                 }
                 live_mask = wave_ballot(has_result);
+                first_pass = false;
                 // variant 8 counts the wave's rays in a scalar (one VGPR less in the hot loop)
                 if (TILED) wave_rays += (uint32_t)__popcll(parked_mask & live_mask);
             }
