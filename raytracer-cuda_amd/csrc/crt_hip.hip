@@ -2220,8 +2220,11 @@ private:
         std::vector<int> queue{0};
         std::vector<crt_sah::Wide> wide;
         prims.clear();
+        // a 4-wide node step costs about one triangle test (the cost probe's weights); node costs 0.5
+        // and 2 measured the same (profiles/r02ax)
+        const crt_sah::Collapse col(bn, 1.0);
         for (size_t qi = 0; qi < queue.size(); ++qi) {
-            const crt_sah::Wide w = crt_sah::open_children(bn, queue[qi]);
+            const crt_sah::Wide w = col.open(queue[qi]);
             wide.push_back(w);
             const int first_child = (int)queue.size();
             for (int s = 0; s < w.n_internal; ++s) queue.push_back(w.bin[s]);

@@ -12,6 +12,7 @@
 // Spheres are always singleton leaves (the kernel's sphere-leaf node).
 #pragma once
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <vector>
@@ -183,43 +184,95 @@ private:
 };
 
 // ---------------------------------------------------------------- 4-wide collapse
-// Each BVH4 node holds the boxes of up to four children.  Children come from the binary tree by
-// repeatedly opening the largest-area internal child (Wald et al., "Getting rid of packets").  Slot
-// order: internal children first (stored at consecutive node indices first_child + slot), then leaf
-// children (their primitives consecutive from leaf_first, in slot order), then empty slots.
+// Each BVH4 node holds the boxes of up to four children, a cut of the binary tree below it (Collapse below).  Slot
+// order: internal children first (stored at consecutive node indices first_child + slot), then leaf children (their
+// primitives consecutive from leaf_first, in slot order), then empty slots.
 struct Wide {
     int n_internal = 0, n_slots = 0;
     int bin[4];          // binary-tree node of each slot
 };
 
-inline Wide open_children(const std::vector<Node>& bn, int n) {
-    Wide w;
-    int c[4], k = 0;
-    if (bn[n].child[0] < 0) {            // a leaf root: one leaf slot
-        c[k++] = n;
-    } else {
-        c[k++] = bn[n].child[0];
-        c[k++] = bn[n].child[1];
-        while (k < 4) {
-            int best = -1;
-            float best_area = -1.f;
-            for (int i = 0; i < k; ++i) {
-                if (bn[c[i]].child[0] < 0) continue;
-                const float a = half_area(bn[c[i]].lo, bn[c[i]].hi);
-                if (a > best_area) { best_area = a; best = i; }
+// SAH-optimal collapse: the cut of the binary tree that forms each 4-wide node, chosen by dynamic programming over
+// the binary tree (Ylitie, Karras, Laine, "Efficient Incoherent Ray Traversal on GPUs Through Compressed Wide BVHs",
+// HPG 2017, without their leaf merging).  Round 2 replaced the greedy collapse (open the largest-area internal child
+// until four slots are used) with it: config C -1.6 %, config E (1M triangles) -9.0 %, the same frames
+// (profiles/r02ax).  Cost of a subtree used as one slot of its parent:
+//   leaf:     A(n) * count(n)                          (one triangle test per primitive, in ray-probability units)
+//   internal: A(n) * c_node + best 4-slot cover of n   (n becomes a 4-wide node: one step, four box tests)
+// cover(n, k) = the cheapest way to cover the subtree of n with at most k slots: n itself as one slot, or (internal n)
+// the covers of its two children with i and k - i slots.  The tree shape does not change which hit a ray reports
+// (closest t, ties to the higher reference rank), only the work to find it.
+class Collapse {
+public:
+    Collapse(const std::vector<Node>& bn, double c_node) : bn_(bn), cover_(bn.size()), split_(bn.size()) {
+        for (int n = (int)bn.size() - 1; n >= 0; --n) {   // children have larger indices than their parent
+            const Node& N = bn[n];
+            const double a = (double)half_area(N.lo, N.hi);
+            auto& c = cover_[n];
+            auto& s = split_[n];
+            if (N.child[0] < 0) {
+                for (int k = 1; k <= 4; ++k) { c[k] = a * N.count; s[k] = 0; }
+                continue;
             }
-            if (best < 0) break;
-            const int x = c[best];
-            c[best] = bn[x].child[0];
-            c[k++] = bn[x].child[1];
+            const int l = N.child[0], r = N.child[1];
+            double open[5];
+            int open_split[5];
+            for (int k = 2; k <= 4; ++k) {
+                open[k] = INFINITY;
+                open_split[k] = 1;
+                for (int i = 1; i < k; ++i) {
+                    const double v = cover_[l][i] + cover_[r][k - i];
+                    if (v < open[k]) { open[k] = v; open_split[k] = i; }
+                }
+            }
+            c[1] = a * c_node + open[4];
+            s[1] = 0;
+            for (int k = 2; k <= 4; ++k) {
+                if (open[k] < c[k - 1]) { c[k] = open[k]; s[k] = open_split[k]; }
+                else { c[k] = c[k - 1]; s[k] = -1; }   // -1: the cover with fewer slots
+            }
         }
     }
-    for (int i = 0; i < k; ++i)
-        if (bn[c[i]].child[0] >= 0) w.bin[w.n_internal++] = c[i];
-    w.n_slots = w.n_internal;
-    for (int i = 0; i < k; ++i)
-        if (bn[c[i]].child[0] < 0) w.bin[w.n_slots++] = c[i];
-    return w;
-}
+
+    // The slots of the 4-wide node made from internal binary node n (a leaf root: one leaf slot).
+    Wide open(int n) const {
+        Wide w;
+        int c[4], k = 0;
+        if (bn_[n].child[0] < 0) {
+            c[k++] = n;
+        } else {
+            // n's own node: its best 4-slot cover, which opens n (split_[n][1] == 0 means "n as one slot" for its
+            // parent; as a node n always opens): the split of open[4] is recomputed from the children's covers
+            const int l = bn_[n].child[0], r = bn_[n].child[1];
+            double best = INFINITY;
+            int bi = 1;
+            for (int i = 1; i < 4; ++i) {
+                const double v = cover_[l][i] + cover_[r][4 - i];
+                if (v < best) { best = v; bi = i; }
+            }
+            gather(l, bi, c, k);
+            gather(r, 4 - bi, c, k);
+        }
+        for (int i = 0; i < k; ++i)
+            if (bn_[c[i]].child[0] >= 0) w.bin[w.n_internal++] = c[i];
+        w.n_slots = w.n_internal;
+        for (int i = 0; i < k; ++i)
+            if (bn_[c[i]].child[0] < 0) w.bin[w.n_slots++] = c[i];
+        return w;
+    }
+
+private:
+    const std::vector<Node>& bn_;
+    std::vector<std::array<double, 5>> cover_;
+    std::vector<std::array<int, 5>> split_;
+
+    void gather(int m, int k, int* c, int& n) const {
+        while (k > 1 && split_[m][k] < 0) --k;
+        if (k == 1 || split_[m][k] == 0) { c[n++] = m; return; }
+        const int i = split_[m][k];
+        gather(bn_[m].child[0], i, c, n);
+        gather(bn_[m].child[1], k - i, c, n);
+    }
+};
 
 }  // namespace crt_sah
