@@ -718,7 +718,10 @@ extern "C" int crt_build_mesh_bvh(int device, const float* positions, uint32_t v
 
 namespace {
 
-constexpr int SAH_BINS = 32;
+#ifndef CRT_SAH_BINS
+#define CRT_SAH_BINS 32
+#endif
+constexpr int SAH_BINS = CRT_SAH_BINS;
 constexpr int SAH_RED = 13 + 3 * SAH_BINS * 7;   // box lo3 hi3, centroid lo3 hi3, spheres; bins: count lo3 hi3
 
 struct SahLevel {

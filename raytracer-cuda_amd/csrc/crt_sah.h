@@ -67,7 +67,10 @@ public:
     int max_depth() const { return max_depth_; }
 
 private:
-    static constexpr int kBins = 32;
+#ifndef CRT_SAH_BINS
+#define CRT_SAH_BINS 32
+#endif
+    static constexpr int kBins = CRT_SAH_BINS;
     std::vector<Item> items_;
     std::vector<Node> nodes_;
     int leaf_size_;
