@@ -106,6 +106,8 @@ def parse():
     ap.add_argument("--no-parity", action="store_true", help="skip the reference-BVH parity frame")
     ap.add_argument("--print-workload-key", action="store_true",
                     help="print the key of profiles/roofline_counters.json for these arguments and exit (tools/pmc.sh)")
+    ap.add_argument("--spatial-splits", action="store_true",
+                    help="rebuilt tree with spatial splits (SBVH, crt_sah::SpatialBuilder; built on the host)")
     ap.add_argument("--host-build", action="store_true",
                     help="build the BVHs on the host (mesh: the sequential restatement of the reference builder; "
                          "rebuilt tree: crt_sah.h) instead of on the GPU")
@@ -279,14 +281,17 @@ def main():
     bvh_desc = "reference (bit-exact)"
     if args.bvh == "rebuilt":
         scene = hs.upload(local, bvh="rebuilt", width=args.bvh_width, leaf_size=args.leaf_size,
-                          traversal_cost=args.traversal_cost, gpu_build=not args.host_build)
-        bvh_desc = (f"rebuilt {args.bvh_width}-wide SAH, leaf<={args.leaf_size}, C_trav={args.traversal_cost:g}")
+                          traversal_cost=args.traversal_cost, gpu_build=not args.host_build,
+                          spatial_splits=args.spatial_splits)
+        bvh_desc = (f"rebuilt {args.bvh_width}-wide SAH, leaf<={args.leaf_size}, C_trav={args.traversal_cost:g}"
+                    + (", spatial splits" if args.spatial_splits else ""))
     t_scene = time.perf_counter() - t
     st = scene.stats()
     counts = hs.counts()
     setup = {"load_build_upload_s": round(t_scene, 3), "load_and_mesh_bvh_s": round(t_load, 3),
              "mesh_bvh_build": "host" if args.host_build else "gpu (crt_build_mesh_bvh)",
-             "rebuilt_bvh_build": "host" if args.host_build else "gpu (binned SAH, crt_scene_options.gpu_build)",
+             "rebuilt_bvh_build": ("host (SBVH)" if args.spatial_splits else "host" if args.host_build
+                                   else "gpu (binned SAH, crt_scene_options.gpu_build)"),
              "mesh_bvh_device_ms": round(hs.device_build_ms(), 2)}
     log_r(f"[scene] {args.scene}: {counts['n_indices'] // 3} triangles, {st['device_nodes']} nodes, "
           f"{st['device_bytes'] / 1e6:.1f} MB in HBM, load+build+upload {t_scene:.2f}s {setup}")
@@ -328,6 +333,7 @@ def main():
     kernel_ms_max = allreduce_max(max(kernel_ms))
     rays_rank = r.counters()["rays"]
     kname = r.last_kernel_name()      # the instantiation the timed frames ran (rocprofv3's spelling)
+    phases = r.last_timings()         # the last timed frame: probe + tile sort, and the main render kernel alone
     [rays_frame] = allreduce_sum_i([rays_rank])
     log_r(f"[timed] {args.steps} frames in {elapsed:.3f}s; render kernel {kernel_ms_avg:.1f} ms avg (rank 0); "
           f"{rays_frame} rays/frame")
@@ -370,8 +376,11 @@ def main():
                                % (st["device_bytes"] / 1e6)}
     ec = roofline_counters(workload_key(args, fr.spp), kname)
     if ec is not None:
-        roofline = roofline_from_counters(ec, rays_rank, kernel_ms_avg / 1e3)
-        roofline.update(kernel=kname, kernel_ms_avg=round(kernel_ms_avg, 3))
+        # the counters are the main render kernel's alone, so they are divided by its own time (HIP events around that
+        # launch only), not by the whole render's, which includes the cost probe and the tile sort
+        roofline = roofline_from_counters(ec, rays_rank, phases["main_kernel_ms"] / 1e3)
+        roofline.update(kernel=kname, kernel_ms=round(phases["main_kernel_ms"], 3),
+                        kernel_ms_note="HIP events around the main render launch of the last timed frame")
     else:
         log_r(f"[roofline] no committed counter summary for {workload_key(args, fr.spp)} / {kname}: roofline null")
 
@@ -427,6 +436,7 @@ def main():
             "rays_per_frame": rays_frame,
             "paths_per_s": round(W * H * args.spp * args.steps / elapsed, 1),
             "render_kernel_ms_avg": round(kernel_ms_avg, 3), "render_kernel_ms_max_over_ranks": round(kernel_ms_max, 3),
+            "render_phases_ms_last_frame": {k: round(v, 3) for k, v in phases.items()},
             "roofline": roofline, "algorithmic": algorithmic, "cpu_baseline": cpu, "parity": parity,
             "setup": setup,
         }

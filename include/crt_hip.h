@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CRT_ABI_VERSION 1
+#define CRT_ABI_VERSION 2
 
 enum crt_status {
     CRT_OK = 0,
@@ -134,6 +134,8 @@ typedef struct crt_scene_stats {
     int64_t excluded_prims;    /* REBUILT: triangles the reference can never hit (zero-thickness boxes) */
     int32_t width;             /* 2 (threaded binary nodes) or 4 (4-wide nodes) */
     int32_t stack_bound;       /* width 4: traversal-stack entries a ray can need */
+    int64_t spatial_splits;    /* REBUILT with spatial_splits: nodes cut by a plane (SBVH) */
+    int64_t references;        /* REBUILT: primitive references in the tree's leaves (> primitives with spatial splits) */
 } crt_scene_stats;
 
 typedef struct crt_work_counters {  /* filled by a CRT_RENDER_COUNT_WORK render */
@@ -152,6 +154,11 @@ typedef struct crt_scene crt_scene;
 typedef struct crt_renderer crt_renderer;
 
 int crt_abi_version(void);
+/* How this library was compiled: CRT_BUILD_CHECKED = the checked build (-DCRT_CHECKED, lib/checked/libcrt_hip.so):
+ * the leaf rounds re-check every (owner, primitive) pair and report a bad one through crt_renderer_synchronize
+ * instead of loading outside the primitive array.  Same frames, slower. */
+#define CRT_BUILD_CHECKED 1
+int crt_build_flags(void);
 const char* crt_last_error(void);   /* thread-local message of the last failing call */
 int crt_device_count(int* out);
 
@@ -172,19 +179,30 @@ typedef struct crt_scene_options {
     int32_t leaf_size;        /* REBUILT: max triangles per leaf, 1..16 (0 = default 4) */
     int32_t layouts;          /* REBUILT: 1 (single left-first order) or 6 (direction-ordered, default) */
     float traversal_cost;     /* REBUILT: SAH cost of one node step relative to one triangle test (0 = default 2) */
-    int32_t width;            /* REBUILT: 4 (default) = 4-wide nodes, stack traversal (kernel variant 4);
+    int32_t width;            /* REBUILT: 4 (default) = 4-wide nodes, stack traversal (kernel variant 4); the
+                                 tree holds at most 2^24 - 1 primitive references (24-bit record addressing in the
+                                 leaf rounds; larger scenes fail with CRT_ERR_INVALID_ARGUMENT);
                                  2 = threaded binary layouts (variants 0-3) */
     int32_t gpu_build;        /* REBUILT: 1 = build the binned-SAH tree on the GPU (crt_scene_create_ex: the scene's
                                  device; crt_scene_export: device 0), 0 = on the host (default) */
     int32_t stack_cap;        /* REBUILT width 4: 0 = the traversal-stack bound computed from the tree (default); > 0
                                  overrides it.  Testing only: a value below the bound makes a render that needs more
                                  entries report CRT_ERR_HIP at synchronisation (the entries are dropped). */
-    int32_t reserved;
+    int32_t spatial_splits;   /* REBUILT: 1 = binned SAH with spatial splits (SBVH, Stich et al. 2009): a primitive
+                                 straddling a split plane is referenced from both sides, each reference boxed by its
+                                 part of the triangle.  Built on the host (gpu_build is ignored).  0 = object splits
+                                 only (default). */
+    float spatial_alpha;      /* spatial_splits: try a spatial split where the object split's children overlap by more
+                                 than this fraction of the root's surface area (0 = default 1e-5) */
+    float spatial_max_dup;    /* spatial_splits: stop splitting once references exceed (1 + this) x primitives
+                                 (0 = default 1.0) */
 } crt_scene_options;
 
 /* ---- scene (SceneManager device half) ---- */
 /* Host-only: build the device arrays crt_scene_create_ex would upload and copy them out (no GPU needed;
- * used by the CPU tests to validate the rebuilt BVH).  Call with null arrays to get the sizes:
+ * used by the CPU tests to validate the rebuilt BVH).  4-wide nodes are returned in their logical row order;
+ * crt_scene_create_ex uploads them swizzled (row k of node n at 16-B slot k ^ (n & 7) of its 128-B record).
+ * Call with null arrays to get the sizes:
  * info = {node float4s, prim float4s, ranks, nodes per layout, layouts, width, stack bound, excluded,
  *         first per-ray sphere prim, per-ray spheres}. */
 int  crt_scene_export(const crt_scene_desc* desc, const crt_scene_options* opts, float* nodes, float* prims,
@@ -281,6 +299,10 @@ uint8_t* crt_renderer_rgba_device_ptr(crt_renderer* r);
 uint32_t* crt_renderer_rng_device_ptr(crt_renderer* r);
 /* Milliseconds of the last render kernel launch(es), measured with HIP events on the launch stream. */
 float crt_renderer_last_kernel_ms(crt_renderer* r);
+/* HIP-event times of the last render, in ms: out[0] = the whole render (== crt_renderer_last_kernel_ms), out[1] = what
+ * runs before the main render kernel (variant 8 / 7: the cost probe and the tile sort; 0 otherwise), out[2] = the main
+ * render kernel alone. */
+int crt_renderer_last_timings(crt_renderer* r, float out[3]);
 /* Template instantiation of the last render-kernel launch as rocprofv3 names it, e.g.
  * "crt_render_kernel<false, 4, 6>" (empty before the first launch and for variant 5). */
 const char* crt_renderer_last_kernel_name(const crt_renderer* r);

@@ -12,11 +12,14 @@ from pathlib import Path
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "liboracle.so"
+# ORACLE_LIB: the sanitizer build (`make -C oracle asan`, tools/run_asan.sh) instead of the in-tree one
+LIB_PATH = Path(os.environ["ORACLE_LIB"]) if os.environ.get("ORACLE_LIB") else HERE / "liboracle.so"
 _lib = None
 
 
 def build(force: bool = False) -> Path:
+    if os.environ.get("ORACLE_LIB"):
+        return LIB_PATH
     if force or not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < (HERE / "crt_oracle.c").stat().st_mtime:
         subprocess.run(["make", "-C", str(HERE), "-B" if force else "liboracle.so"], check=True,
                        stdout=subprocess.DEVNULL)

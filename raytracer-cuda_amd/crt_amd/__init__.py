@@ -109,15 +109,17 @@ class HostScene:
         return idx, fm
 
     def upload(self, device: int = 0, bvh: str = "reference", leaf_size: int = 0, layouts: int = 0,
-               traversal_cost: float = 0.0, width: int = 0, gpu_build: bool = False, stack_cap: int = 0) -> "Scene":
+               traversal_cost: float = 0.0, width: int = 0, gpu_build: bool = False, stack_cap: int = 0,
+               spatial_splits: bool = False, spatial_alpha: float = 0.0, spatial_max_dup: float = 0.0) -> "Scene":
         """Device scene.  bvh="reference": the reference's BVHs, bit-exact (crth_scene_upload);
         bvh="rebuilt": binned-SAH BVH with the reference's hit rule (crt_scene_create_ex)."""
         h = C.c_void_p()
         if (bvh == "reference" and not leaf_size and not layouts and not traversal_cost and not width and not gpu_build
-                and not stack_cap):
+                and not stack_cap and not spatial_splits):
             check_host(_lib.host().crth_scene_upload(self.h, int(device), C.byref(h)), "crth_scene_upload")
             return Scene(h, device)
-        o = scene_options(bvh, leaf_size, layouts, traversal_cost, width, gpu_build, stack_cap)
+        o = scene_options(bvh, leaf_size, layouts, traversal_cost, width, gpu_build, stack_cap, spatial_splits,
+                          spatial_alpha, spatial_max_dup)
         d = self.desc()
         check(_lib.hip().crt_scene_create_ex(C.byref(d), int(device), C.byref(o), C.byref(h)), "crt_scene_create_ex")
         return Scene(h, device)
@@ -141,7 +143,8 @@ class HostScene:
 
 
 def scene_options(bvh: str = "reference", leaf_size: int = 0, layouts: int = 0, traversal_cost: float = 0.0,
-                  width: int = 0, gpu_build: bool = False, stack_cap: int = 0):
+                  width: int = 0, gpu_build: bool = False, stack_cap: int = 0, spatial_splits: bool = False,
+                  spatial_alpha: float = 0.0, spatial_max_dup: float = 0.0):
     modes = {"reference": _lib.BVH_REFERENCE, "rebuilt": _lib.BVH_REBUILT}
     if bvh not in modes:
         raise ValueError(f"bvh must be one of {sorted(modes)}")
@@ -151,6 +154,9 @@ def scene_options(bvh: str = "reference", leaf_size: int = 0, layouts: int = 0, 
     o.width = int(width)
     o.gpu_build = int(bool(gpu_build))
     o.stack_cap = int(stack_cap)
+    o.spatial_splits = int(bool(spatial_splits))
+    o.spatial_alpha = float(spatial_alpha)
+    o.spatial_max_dup = float(spatial_max_dup)
     return o
 
 
@@ -286,6 +292,13 @@ class Renderer:
 
     def last_kernel_name(self) -> str:
         return (_lib.hip().crt_renderer_last_kernel_name(self.h) or b"").decode()
+
+    def last_timings(self) -> dict:
+        """HIP-event ms of the last render: the whole render, the probe + tile sort before the main kernel, and the
+        main render kernel alone (crt_renderer_last_timings)."""
+        a = (C.c_float * 3)()
+        check(_lib.hip().crt_renderer_last_timings(self.h, a), "last_timings")
+        return {"render_ms": float(a[0]), "probe_sort_ms": float(a[1]), "main_kernel_ms": float(a[2])}
 
     def last_kernel_ms(self) -> float:
         return float(_lib.hip().crt_renderer_last_kernel_ms(self.h))

@@ -16,7 +16,8 @@ REPO = PKG_ROOT.parent
 LIB_DIR = PKG_ROOT / "lib"
 # CRT_HIP_LIB: an alternative build of the same library (A/B profiling builds, tools/); default in-tree
 HIP_LIB = Path(os.environ["CRT_HIP_LIB"]) if os.environ.get("CRT_HIP_LIB") else LIB_DIR / "libcrt_hip.so"
-HOST_LIB = LIB_DIR / "libcrt_host.so"
+# CRT_HOST_LIB: an alternative build of the host library (the sanitizer build, `make asan`, tools/run_asan.sh)
+HOST_LIB = Path(os.environ["CRT_HOST_LIB"]) if os.environ.get("CRT_HOST_LIB") else LIB_DIR / "libcrt_host.so"
 
 
 class CrtError(RuntimeError):
@@ -71,17 +72,21 @@ class MaterialDesc(C.Structure):      # crt_hip.h crt_material_desc
 class SceneStats(C.Structure):
     _fields_ = [("device_nodes", C.c_int64), ("device_prims", C.c_int64), ("device_bytes", C.c_int64),
                 ("max_depth", C.c_int32), ("n_materials", C.c_int32), ("bvh", C.c_int32), ("layouts", C.c_int32),
-                ("excluded_prims", C.c_int64), ("width", C.c_int32), ("stack_bound", C.c_int32)]
+                ("excluded_prims", C.c_int64), ("width", C.c_int32), ("stack_bound", C.c_int32),
+                ("spatial_splits", C.c_int64), ("references", C.c_int64)]
 
 
 class SceneOptions(C.Structure):
     _fields_ = [("bvh", C.c_int32), ("leaf_size", C.c_int32), ("layouts", C.c_int32),
                 ("traversal_cost", C.c_float), ("width", C.c_int32), ("gpu_build", C.c_int32),
-                ("stack_cap", C.c_int32), ("reserved", C.c_int32)]
+                ("stack_cap", C.c_int32), ("spatial_splits", C.c_int32),
+                ("spatial_alpha", C.c_float), ("spatial_max_dup", C.c_float)]
 
 
 BVH_REFERENCE = 0
 BVH_REBUILT = 1
+ABI_VERSION = 2          # include/crt_hip.h CRT_ABI_VERSION
+BUILD_CHECKED = 1        # crt_build_flags(): the -DCRT_CHECKED build
 
 
 class WorkCounters(C.Structure):
@@ -91,14 +96,14 @@ class WorkCounters(C.Structure):
 
 # exported symbol lists (checked by tests against include/*.h)
 HIP_SYMBOLS = [
-    "crt_abi_version", "crt_last_error", "crt_device_count", "crt_scene_create", "crt_scene_create_ex", "crt_scene_get_stats", "crt_scene_compare", "crt_scene_compare_dump", "crt_scene_export",
+    "crt_abi_version", "crt_build_flags", "crt_last_error", "crt_device_count", "crt_scene_create", "crt_scene_create_ex", "crt_scene_get_stats", "crt_scene_compare", "crt_scene_compare_dump", "crt_scene_export",
     "crt_renderer_set_stack_lds", "crt_renderer_get_section_profile", "crt_renderer_get_section_profile_ex",
     "crt_scene_destroy", "crt_renderer_create", "crt_renderer_destroy", "crt_renderer_init_rand",
     "crt_renderer_set_camera", "crt_renderer_render", "crt_renderer_resolve", "crt_renderer_render_frame",
     "crt_renderer_synchronize", "crt_renderer_read_linear", "crt_renderer_read_rgba8", "crt_renderer_read_rng",
     "crt_renderer_write_linear", "crt_renderer_get_counters", "crt_renderer_linear_device_ptr",
     "crt_renderer_rgba_device_ptr", "crt_renderer_rng_device_ptr", "crt_renderer_last_kernel_ms",
-    "crt_renderer_last_kernel_name",
+    "crt_renderer_last_kernel_name", "crt_renderer_last_timings",
     "crt_renderer_attach_linear", "crt_renderer_set_kernel_variant", "crt_renderer_get_schedule_stats",
     "crt_renderer_set_regen_threshold", "crt_renderer_set_occupancy_target",
     "crt_build_mesh_bvh", "crt_renderer_set_schedule", "crt_renderer_set_critical_tiles",
@@ -140,7 +145,7 @@ def hip():
         L = C.CDLL(str(HIP_LIB), mode=C.RTLD_GLOBAL)
         P, i32, u64, f32 = C.c_void_p, C.c_int, C.c_ulonglong, C.c_float
         sig = {
-            "crt_abi_version": ([], i32), "crt_last_error": ([], C.c_char_p),
+            "crt_abi_version": ([], i32), "crt_build_flags": ([], i32), "crt_last_error": ([], C.c_char_p),
             "crt_device_count": ([P], i32),
             "crt_scene_create": ([P, i32, P], i32), "crt_scene_create_ex": ([P, i32, P, P], i32),
             "crt_scene_compare": ([P, P, P, i32, i32, P], i32),
@@ -154,7 +159,7 @@ def hip():
             "crt_renderer_init_rand": ([P, u64, u64, P], i32), "crt_renderer_set_camera": ([P, P], i32),
             "crt_renderer_render": ([P, P, i32, i32, C.c_uint, P], i32),
             "crt_renderer_resolve": ([P, f32, P], i32), "crt_renderer_render_frame": ([P, P, P], i32),
-            "crt_renderer_synchronize": ([P, P], i32),
+            "crt_renderer_synchronize": ([P, P], i32), "crt_renderer_last_timings": ([P, P], i32),
             "crt_renderer_read_linear": ([P, P], i32), "crt_renderer_read_rgba8": ([P, P], i32),
             "crt_renderer_read_rng": ([P, P], i32), "crt_renderer_write_linear": ([P, P], i32),
             "crt_renderer_get_counters": ([P, P], i32),
@@ -183,6 +188,9 @@ def hip():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
+        if L.crt_abi_version() != ABI_VERSION and not os.environ.get("CRT_HIP_LIB"):
+            raise CrtError(f"{HIP_LIB}: C ABI version {L.crt_abi_version()}, these bindings expect {ABI_VERSION} "
+                           "(rebuild the library)")
         _hip = L
     return _hip
 

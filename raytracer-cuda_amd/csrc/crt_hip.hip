@@ -272,9 +272,17 @@ __device__ __forceinline__ int wave_inclusive_scan_shfl(int x, int lane) {
 struct WaveLds {
     float4 ray0[64];                 // o.x, o.y, o.z, d.x of each lane's ray
     float4 ray1[64];                 // d.y, d.z, closest at leaf entry, first prim (int bits)
+#ifdef CRT_LEAF_DUMMY
+    unsigned long long key[128];     // per owner: (t bits << 32) | (0xffffffff - rank), min-reduced; 64..127: per-lane
+                                     // sinks for the rejected pairs' atomics
+#else
     unsigned long long key[64];      // per owner: (t bits << 32) | (0xffffffff - rank), min-reduced
+#endif
     int prefix[64];                  // first pair index of each owner's leaf
     unsigned char owner_at[64];      // owner lane of the pair that starts at each slot of a round
+#ifdef CRT_CHECKED
+    int span_n[64];                  // checked build: each owner's pair count (its first pair is prefix[owner])
+#endif
 };
 
 // Möller–Trumbore (Mesh.cuh:266-308) on a triangle record; returns t or -1 when rejected (any accepted
@@ -890,7 +898,7 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
             leaf_first = __float_as_int(mf.z) + lo;
             // the span must lie inside the primitive array: checked here once per lane and step instead of per pair
             // in the leaf rounds (-0.7 %, profiles/r02v); a corrupt node reports through P.err and tests nothing
-            if ((unsigned)(leaf_first + leaf_n) > (unsigned)P.n_prims) {
+            if ((unsigned)leaf_first > (unsigned)P.n_prims || (unsigned)leaf_n > (unsigned)(P.n_prims - leaf_first)) {
                 atomicOr(P.err, 1u);
                 leaf_n = 0;
             }
@@ -959,6 +967,10 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         // leaf_first - prefix: a pair's primitive is ray1.w + its index j (-0.27 %, profiles/r02aq; round 1 measured
         // this +2.2 %, profiles/r01aj, before the round-2 changes to the round's code)
         L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first - pfx));
+#ifdef CRT_CHECKED
+        L.prefix[lane] = pfx;
+        L.span_n[lane] = leaf_n;
+#endif
         // the empty key, materialised here: as a plain constant the register allocator keeps ~0ull live across
         // the loop and spills it (a scratch reload and a vmcnt(0) wait on every leaf step)
         uint32_t ones;
@@ -980,12 +992,32 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
             const int p = __float_as_int(r1.w) + j;   // leaf_first - prefix + j: inside the owner's checked span
             if (COUNT) cnt.tris++;
             int rank;
+#ifdef CRT_CHECKED
+            // checked build (-DCRT_CHECKED, lib/checked/): the per-pair bounds the fast path proves once per lane and
+            // step (node_step4), re-checked here with the owner lookup itself, so a stale LDS owner mark or a wrong
+            // prefix reports through P.err instead of loading outside the primitive array
+            const bool bad = (unsigned)owner >= 64u || j < L.prefix[owner] || j >= L.prefix[owner] + L.span_n[owner] ||
+                             (unsigned)p >= (unsigned)P.n_prims;
+            if (bad) atomicOr(P.err, 4u);
+            rank = -1;
+            const float t = bad ? -1.f : prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
+                                                   P.tree_spheres != 0);
+#else
             const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
                                       P.tree_spheres != 0);
+#endif
             // a rejected pair offers the empty key (no effect on the min): one LDS atomic per pair, no branch
             // (-0.75 %, profiles/r02ar)
             const unsigned long long kp = ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank);
+#ifdef CRT_LEAF_DUMMY
+            atomicMin(&L.key[t >= 0.f ? owner : 64 + lane], kp);
+#elif defined(CRT_LEAF_SELF)
+            // a rejected pair offers the empty key at its own lane's slot (a no-op min on a distinct address), so only
+            // the accepted pairs of one owner contend for the owner's word
+            atomicMin(&L.key[t >= 0.f ? owner : lane], t >= 0.f ? kp : ~0ull);
+#else
             atomicMin(&L.key[owner], t >= 0.f ? kp : ~0ull);
+#endif
         }
         carry = __builtin_amdgcn_readlane(owner1, 63);
         wave_sync();
@@ -2099,20 +2131,39 @@ struct Rebuilt {
     static constexpr int kMaxRaySpheres = 8;
 
     // gpu_device >= 0: the binned-SAH tree is built on that GPU (crtx_build_sah_gpu, crt_bvh_build.hip)
-    bool build(const Flattener& F, int leaf_size, int layouts, float trav_cost, int wide, int gpu_device = -1) {
+    long spatial_splits = 0;   // SBVH: nodes cut by a plane, and primitive references in the leaves
+    long references = 0;
+
+    // gpu_device >= 0: the binned-SAH tree is built on that GPU (crtx_build_sah_gpu, crt_bvh_build.hip); spatial:
+    // SBVH on the host (crt_sah::SpatialBuilder), width 4 only
+    bool build(const Flattener& F, int leaf_size, int layouts, float trav_cost, int wide, int gpu_device = -1,
+               bool spatial = false, float alpha = 1e-5f, float max_dup = 1.f) {
         width = wide;
         const int n = (int)(F.prims.size() / 3);
         std::vector<crt_sah::Item> items;
         items.reserve(n);
         std::vector<int> ray_sph;
+        std::vector<crt_sah::TriVerts> verts;
+        if (spatial && width != 4) { err = "spatial splits need width 4"; return false; }
         int n_sph = 0;
         for (int p = 0; p < n; ++p) n_sph += (F.rank_code[F.rank_of[p]] & SPHERE_BIT) != 0;
         const bool spheres_per_ray = width == 4 && n_sph <= kMaxRaySpheres;
         for (int p = 0; p < n; ++p) {
             const bool sphere = (F.rank_code[F.rank_of[p]] & SPHERE_BIT) != 0;
             if (!F.reachable[p]) { excluded += !sphere; continue; }
-            if (sphere && spheres_per_ray) { ray_sph.push_back(p); continue; }
             const float4 f0 = F.prims[3 * p], f1 = F.prims[3 * p + 1], f2 = F.prims[3 * p + 2];
+            if (sphere && spheres_per_ray) {
+                // a per-ray sphere's hit point becomes a ray origin too: the same 2^60 bound as the tree's boxes
+                // (wide_boxes: |o| * 2^64 must stay finite)
+                const float c[3] = {f0.x, f0.y, f0.z}, r = std::fabs(f0.w);
+                for (int a = 0; a < 3; ++a)
+                    if (!(std::fabs(c[a] - r) < 0x1p60f && std::fabs(c[a] + r) < 0x1p60f)) {
+                        err = "sphere bounds non-finite or beyond 2^60";
+                        return false;
+                    }
+                ray_sph.push_back(p);
+                continue;
+            }
             crt_sah::Item it;
             it.src = p;
             it.sphere = sphere;
@@ -2127,6 +2178,18 @@ struct Rebuilt {
                     it.lo[a] = std::min(v0[a], std::min(v1, v2));
                     it.hi[a] = std::max(v0[a], std::max(v1, v2));
                 }
+            }
+            if (spatial && !sphere) {   // the triangle's vertices for clipping, v0 + e1 and v0 + e2 exact in double
+                crt_sah::TriVerts T;
+                const double v0[3] = {f0.x, f0.y, f0.z};
+                const double e1[3] = {f0.w, f1.x, f1.y}, e2[3] = {f1.z, f1.w, f2.x};
+                for (int a = 0; a < 3; ++a) {
+                    T.v[0][a] = v0[a];
+                    T.v[1][a] = v0[a] + e1[a];
+                    T.v[2][a] = v0[a] + e2[a];
+                }
+                it.tri = (int)verts.size();
+                verts.push_back(T);
             }
             bool finite = true;
             for (int a = 0; a < 3; ++a) {
@@ -2177,7 +2240,14 @@ struct Rebuilt {
         }
         std::vector<crt_sah::Node> bnv;
         std::vector<crt_sah::Item> its;
-        if (gpu_device >= 0) {
+        if (spatial) {
+            crt_sah::SpatialBuilder B(std::move(items), std::move(verts), leaf_size, trav_cost, alpha, max_dup);
+            B.build();
+            max_depth = B.max_depth();
+            spatial_splits = B.spatial_splits();
+            bnv = B.nodes();
+            its = B.items();
+        } else if (gpu_device >= 0) {
             std::vector<int> order;
             if (crtx_build_sah_gpu(gpu_device, items, leaf_size, trav_cost, &bnv, &order, &max_depth) != CRT_OK) {
                 err = std::string("GPU SAH build: ") + crt_last_error();
@@ -2192,6 +2262,7 @@ struct Rebuilt {
             bnv = B.nodes();
             its = B.items();
         }
+        references = (long)its.size();
         if (width == 4) {
             if (!emit4(F, bnv, its)) return false;
             append_ray_spheres();
@@ -2317,6 +2388,7 @@ struct crt_scene {
     int bvh = CRT_BVH_REFERENCE, layouts = 1;
     int width = 2;                 // 2: threaded layouts (variants 0-3); 4: 4-wide nodes (variant 4)
     int stack_cap = 0;             // width 4: traversal-stack entries a ray can need
+    long spatial_splits = 0, references = 0;   // rebuilt tree: SBVH cuts, leaf references
     int sphere_first = 0, n_ray_spheres = 0;   // width 4: spheres tested per ray, prims [first, first + n)
     float sph2[2][12] = {};                    // width 4 with exactly two per-ray spheres: their kernel-argument copy
     int tree_spheres = 1;                      // width 4: some leaf holds a sphere
@@ -2336,6 +2408,7 @@ struct crt_renderer {
     crt_camera_desc cam{};
     bool has_camera = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_main = nullptr;  // recorded just before the main render kernel (after the cost probe and tile sort)
     bool timed = false;
     char kernel_name[64] = "";     // instantiation of the last render launch, rocprof's spelling
     // variant 7: pixel order, slot queue, probe costs, sort scratch (allocated on first use)
@@ -2382,6 +2455,13 @@ int use_device(int dev) {
 extern "C" {
 
 int crt_abi_version(void) { return CRT_ABI_VERSION; }
+int crt_build_flags(void) {
+#ifdef CRT_CHECKED
+    return CRT_BUILD_CHECKED;
+#else
+    return 0;
+#endif
+}
 const char* crt_last_error(void) { return g_last_error.c_str(); }
 
 int crt_device_count(int* out) {
@@ -2419,7 +2499,13 @@ static int build_scene_arrays(const crt_scene_desc* D, const crt_scene_options* 
     F.finalize_ranks();
     if (o.bvh == CRT_BVH_REBUILT) {
         if (o.width == 4) o.layouts = 1;
-        if (!RB.build(F, o.leaf_size, o.layouts, o.traversal_cost, o.width, o.gpu_build ? gpu_device : -1))
+        if (o.spatial_alpha == 0.f) o.spatial_alpha = 1e-5f;
+        if (o.spatial_max_dup == 0.f) o.spatial_max_dup = 1.f;
+        if (o.spatial_splits != 0 && o.spatial_splits != 1) return set_error(CRT_ERR_INVALID_ARGUMENT, "spatial_splits must be 0 or 1");
+        if (!(o.spatial_alpha > 0.f && o.spatial_alpha <= 1.f) || !(o.spatial_max_dup > 0.f && o.spatial_max_dup <= 8.f))
+            return set_error(CRT_ERR_INVALID_ARGUMENT, "spatial_alpha must be in (0, 1], spatial_max_dup in (0, 8]");
+        if (!RB.build(F, o.leaf_size, o.layouts, o.traversal_cost, o.width, o.gpu_build && !o.spatial_splits ? gpu_device : -1,
+                      o.spatial_splits != 0, o.spatial_alpha, o.spatial_max_dup))
             return set_error(CRT_ERR_INVALID_ARGUMENT, "scene: " + RB.err);
         if ((size_t)RB.n_nodes * o.layouts * (o.width == 4 ? 8 : 2) >= (size_t)1 << 31)
             return set_error(CRT_ERR_INVALID_ARGUMENT, "scene too large");
@@ -2539,6 +2625,8 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
     S->width = rebuilt ? RB.width : 2;
     S->stack_cap = rebuilt ? (o.stack_cap > 0 ? o.stack_cap : RB.stack_bound) : 0;
     S->sphere_first = rebuilt ? RB.sphere_first : 0;
+    S->spatial_splits = rebuilt ? RB.spatial_splits : 0;
+    S->references = rebuilt ? RB.references : 0;
     {
         int in_tree = 0;   // spheres the 4-wide tree itself holds (not tested per ray)
         if (rebuilt)
@@ -2590,6 +2678,8 @@ int crt_scene_get_stats(const crt_scene* S, crt_scene_stats* out) {
     out->device_nodes = (int64_t)S->n_nodes * S->layouts;
     out->width = S->width;
     out->stack_bound = S->stack_cap;
+    out->spatial_splits = S->spatial_splits;
+    out->references = S->references;
     out->device_prims = S->n_prims;
     out->device_bytes = (int64_t)S->n_nodes * S->layouts * (S->width == 4 ? 128 : 32) + (int64_t)S->n_prims * 48 + (int64_t)S->n_mats * 48 +
                         (int64_t)S->n_ranks * 48;
@@ -2660,7 +2750,8 @@ int crt_renderer_create(int width, int height, int device, crt_renderer** out) {
         (e = hipMemset(R->d_sum_own, 0, n * 3 * 4)) != hipSuccess ||
         (e = hipMemset(R->d_rgba, 0, n * 4)) != hipSuccess ||
         (e = hipMemset(R->d_counters, 0, 16 * sizeof(unsigned long long))) != hipSuccess ||
-        (e = hipEventCreate(&R->ev0)) != hipSuccess || (e = hipEventCreate(&R->ev1)) != hipSuccess) {
+        (e = hipEventCreate(&R->ev0)) != hipSuccess || (e = hipEventCreate(&R->ev1)) != hipSuccess ||
+        (e = hipEventCreate(&R->ev_main)) != hipSuccess) {
         crt_renderer_destroy(R);
         return set_error(e == hipErrorOutOfMemory ? CRT_ERR_OUT_OF_MEMORY : CRT_ERR_HIP,
                          std::string("renderer allocation: ") + hipGetErrorString(e));
@@ -2710,6 +2801,7 @@ void crt_renderer_destroy(crt_renderer* R) {
     if (R->d_rng_cache) (void)hipFree(R->d_rng_cache);
     if (R->ev0) (void)hipEventDestroy(R->ev0);
     if (R->ev1) (void)hipEventDestroy(R->ev1);
+    if (R->ev_main) (void)hipEventDestroy(R->ev_main);
     delete R;
 }
 
@@ -2829,6 +2921,8 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     std::memcpy(P.sph2, S->sph2, sizeof P.sph2);
     const int occ = R->min_waves ? R->min_waves : (S->width == 4 ? 6 : 5);
     P.stack_lds = std::min(R->stack_lds, occ >= 7 ? 11 : occ >= 6 ? 12 : STACK_LDS);
+    // a stack_cap override below the LDS entries must still report the entries it drops (crt_scene_options.stack_cap)
+    if (S->width == 4 && S->stack_cap > 0) P.stack_lds = std::min(P.stack_lds, S->stack_cap);
     if (S->width == 4 && S->stack_cap > P.stack_lds) {
         const size_t need = (size_t)(S->stack_cap - P.stack_lds);
         if (need * R->width * R->height * 4 >= ((size_t)1 << 32))
@@ -2851,6 +2945,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     do {                                                                                     \
         std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, %d, %d>", \
                       cnt ? "true" : "false", V, W);                                         \
+        HIP_TRY(hipEventRecord(R->ev_main, st));                                             \
         if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, V, W>), grid, block, 0, st, P);  \
         else hipLaunchKernelGGL((crt_render_kernel<false, V, W>), grid, block, 0, st, P);     \
     } while (0)
@@ -2902,6 +2997,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         }
         const dim3 tgrid(n_tiles), tblock(64);
         const char* cs = cnt ? "true" : "false";
+        HIP_TRY(hipEventRecord(R->ev_main, st));
         if (occ >= 7) {
             std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 8, 7>", cs);
             if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 8, 7>), tgrid, tblock, 0, st, P);
@@ -2955,6 +3051,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         const int per_cu = occ >= 7 ? 7 : occ >= 6 ? 6 : 5;        // workgroups of 4 waves resident per CU
         const int n_wg = std::max(1, std::min(R->n_cus * per_cu, (int)((n_pix + 255) / 256)));
         const dim3 pgrid(n_wg);
+        HIP_TRY(hipEventRecord(R->ev_main, st));
         if (occ >= 7) {
             std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 7, 7>", cnt ? "true" : "false");
             if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 7, 7>), pgrid, block, 0, st, P);
@@ -3077,6 +3174,7 @@ static int take_device_error(crt_renderer* R, unsigned long long word) {
     std::string m = "render kernel reported an internal error:";
     if (word & 1u) m += " primitive index out of range;";
     if (word & 2u) m += " traversal stack deeper than the scene's stack bound (entries dropped);";
+    if (word & 4u) m += " leaf-round pair outside its owner's span (checked build);";
     return set_error(CRT_ERR_HIP, m + " the frame is invalid");
 }
 
@@ -3163,6 +3261,17 @@ extern "C" int crt_profile_wave_times(unsigned long long* out, int n_waves) {
     return CRT_OK;
 }
 #endif
+
+int crt_renderer_last_timings(crt_renderer* R, float out[3]) {
+    if (!R || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    if (!R->timed) return set_error(CRT_ERR_INVALID_ARGUMENT, "no render yet");
+    HIP_TRY(hipSetDevice(R->device));
+    HIP_TRY(hipEventSynchronize(R->ev1));
+    HIP_TRY(hipEventElapsedTime(&out[0], R->ev0, R->ev1));
+    HIP_TRY(hipEventElapsedTime(&out[1], R->ev0, R->ev_main));
+    HIP_TRY(hipEventElapsedTime(&out[2], R->ev_main, R->ev1));
+    return CRT_OK;
+}
 
 float crt_renderer_last_kernel_ms(crt_renderer* R) {
     if (!R || !R->timed) return -1.f;

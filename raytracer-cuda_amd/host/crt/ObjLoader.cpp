@@ -71,8 +71,9 @@ bool TryParseDouble(const char* s, const char* s_end, double* result) {
         read = 0;
         end_not_reached = (curr != s_end);
         while (end_not_reached && is_digit(*curr)) {
-            exponent *= 10;
-            exponent += static_cast<int>(*curr - 0x30);
+            // tinyobjloader lets the int overflow (undefined behaviour, found by UBSan in tools/run_asan.sh); any
+            // exponent beyond 9999 already makes the value inf or 0, so it stops growing there
+            if (exponent < 100000) exponent = exponent * 10 + static_cast<int>(*curr - 0x30);
             curr++;
             read++;
             end_not_reached = (curr != s_end);

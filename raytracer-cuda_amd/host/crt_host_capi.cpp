@@ -112,9 +112,10 @@ int crth_scene_counts(const crth_scene* s, int64_t* c) {
 int crth_scene_loader_arrays(const crth_scene* s, float* pos, uint32_t* idx, int32_t* fm, uint32_t* info, float* mats) {
     if (!s) { g_err = "bad argument"; return CRT_ERR_INVALID_ARGUMENT; }
     const auto& P = s->sm.positions();
-    if (pos) std::memcpy(pos, P.data(), P.size() * sizeof(float));
-    if (idx) std::memcpy(idx, s->idx0.data(), s->idx0.size() * sizeof(uint32_t));
-    if (fm) std::memcpy(fm, s->fmat0.data(), s->fmat0.size() * sizeof(int32_t));
+    // (an empty vector's data() may be null, and memcpy from null is undefined even for 0 bytes: UBSan, tools/run_asan.sh)
+    if (pos && !P.empty()) std::memcpy(pos, P.data(), P.size() * sizeof(float));
+    if (idx && !s->idx0.empty()) std::memcpy(idx, s->idx0.data(), s->idx0.size() * sizeof(uint32_t));
+    if (fm && !s->fmat0.empty()) std::memcpy(fm, s->fmat0.data(), s->fmat0.size() * sizeof(int32_t));
     if (info) {
         const auto& M = s->sm.meshes();
         for (size_t i = 0; i < M.size(); ++i) {

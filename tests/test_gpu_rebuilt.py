@@ -16,7 +16,8 @@ pytestmark = pytest.mark.gpu
 RMS_TOL = 1e-4
 
 CONFIGS = {"w4": dict(width=4), "w4l8": dict(width=4, leaf_size=8, traversal_cost=2),
-           "w2l16": dict(width=2, leaf_size=16, traversal_cost=6)}
+           "w2l16": dict(width=2, leaf_size=16, traversal_cost=6),
+           "w4sbvh": dict(width=4, spatial_splits=True)}   # spatial splits: triangles referenced from several leaves
 
 
 @pytest.fixture(scope="module")
@@ -54,6 +55,12 @@ def test_rebuilt_stats(rebuilt, device_scenes):
     for k, opts in CONFIGS.items():
         st = rebuilt["cornell_bunny", k].stats()
         assert st["bvh"] == 1 and st["width"] == opts["width"]
+        if opts.get("spatial_splits"):   # straddling triangles are referenced from both sides of a spatial split
+            plain = rebuilt["cornell_bunny", "w4"].stats()
+            assert st["spatial_splits"] > 0 and st["device_prims"] > plain["device_prims"]
+            assert st["references"] == st["device_prims"] - 2          # the two per-ray spheres are not in leaves
+            continue
+        assert st["spatial_splits"] == 0
         assert st["device_prims"] + st["excluded_prims"] == ref["device_prims"]
         if opts["width"] == 4:
             assert st["stack_bound"] > 1

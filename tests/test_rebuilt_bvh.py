@@ -324,3 +324,99 @@ def test_ground_sphere_box_culls_spurious_root():
         tmin = max(max(min(t0[0], t1[0]), min(t0[1], t1[1])), min(t0[2], t1[2]), F32(0.001))
         tmax = min(max(t0[0], t1[0]), max(t0[1], t1[1]), max(t0[2], t1[2]))
         assert tmax <= tmin, "the reference's sphere box test rejects the ray"
+
+
+# ---------------------------------------------------------------- spatial splits (SBVH, crt_sah::SpatialBuilder)
+@pytest.fixture(scope="module")
+def sbvh_export(host_scene):
+    return host_scene.export("rebuilt", width=4, spatial_splits=True)
+
+
+def _wide_leaves(e):
+    """(slot lo, slot hi, first prim, count) of every leaf slot of a 4-wide export."""
+    nodes = e["nodes"].reshape(-1, 8, 4)
+    out = []
+    for q in nodes:
+        fc, meta, lf, counts = _i(q[6])
+        n_int, n_slots = meta & 0xFF, meta >> 8
+        off = 0
+        for s in range(4):
+            c = (counts >> (8 * s)) & 0xFF
+            if n_int <= s < n_slots:
+                lo = np.array([q[0, s], q[2, s], q[4, s]], np.float64)
+                hi = np.array([q[1, s], q[3, s], q[5, s]], np.float64)
+                out.append((lo, hi, lf + off, c))
+            off += c
+    return out
+
+
+def test_sbvh_structure(host_scene, ref_export, sbvh_export):
+    """Every reachable primitive is referenced at least once (straddling ones more than once), every reference is
+    the reference scene's record with the same rank, and the references of a triangle cover it: sample points of
+    every split triangle lie inside one of its leaves' boxes."""
+    e = sbvh_export
+    plain = host_scene.export("rebuilt", width=4)
+    prims = e["prims"].reshape(-1, 3, 4)
+    ranks = _prim_ranks(e["prims"])
+    n_tree = e["sphere_first"]
+    uniq, cnt = np.unique(ranks[:n_tree], return_counts=True)
+    assert len(uniq) + e["n_ray_spheres"] + e["excluded"] == ref_export["ranks"]
+    assert len(uniq) == plain["sphere_first"]
+    assert (cnt > 1).sum() > 0, "the benchmark scene has straddling triangles"
+    assert n_tree <= 2 * len(uniq)
+    ref_prims = ref_export["prims"].reshape(-1, 3, 4)
+    ref_idx = ref_export["rank_code"][ranks[:n_tree]] & ~(1 << 30)
+    assert np.array_equal(prims[:n_tree].view(np.uint32), ref_prims[ref_idx].view(np.uint32))
+    boxes = {}
+    for lo, hi, first, c in _wide_leaves(e):
+        for p in range(first, first + c):
+            boxes.setdefault(int(ranks[p]), []).append((lo, hi))
+    rng = np.random.default_rng(11)
+    split = uniq[cnt > 1]
+    check = np.concatenate([split, rng.choice(uniq, 200, replace=False)])
+    for r in check:
+        rec = prims[np.nonzero(ranks == r)[0][0]].astype(np.float64)
+        v0 = rec[0, :3]
+        e1 = np.array([rec[0, 3], rec[1, 0], rec[1, 1]])
+        e2 = np.array([rec[1, 2], rec[1, 3], rec[2, 0]])
+        uv = rng.uniform(size=(64, 2))
+        uv = np.where(uv.sum(1, keepdims=True) > 1, 1 - uv, uv)
+        pts = np.concatenate([v0 + uv[:, :1] * e1 + uv[:, 1:] * e2, [v0, v0 + e1, v0 + e2]])
+        inside = np.zeros(len(pts), bool)
+        for lo, hi in boxes[int(r)]:
+            inside |= ((pts >= lo) & (pts <= hi)).all(1)
+        assert inside.all(), f"rank {r}: part of the triangle is outside every leaf box of its references"
+    # the leaf boxes of references still strictly enclose unsplit triangles
+    for lo, hi, first, c in _wide_leaves(e)[:2000]:
+        for p in range(first, first + c):
+            if cnt[np.searchsorted(uniq, ranks[p])] == 1:
+                plo, phi = _prim_box(prims[p])
+                assert (plo > lo).all() and (phi < hi).all()
+
+
+def test_sbvh_traversal_equals_brute_force(host_scene, sbvh_export):
+    e = sbvh_export
+    prims = e["prims"].reshape(-1, 3, 4)
+    ranks = _prim_ranks(e["prims"])
+    rng = np.random.default_rng(7)
+    n_hit = 0
+    for i in range(160):
+        if i % 2:
+            o = rng.uniform([-0.25, 0.0, -0.25], [0.25, 0.5, 0.25]).astype(np.float32)
+            tgt = np.array([-0.096, 0.14, -0.078], np.float32) + rng.normal(0, 0.04, 3).astype(np.float32)
+            d = (tgt - o).astype(np.float32)
+        else:
+            o = rng.uniform([-0.27, 0.01, -0.27], [0.27, 0.54, 0.3]).astype(np.float32)
+            d = rng.normal(size=3).astype(np.float32)
+        brute = _best(_prim_t(prims, o, d, np.float32(np.inf)), ranks)
+        got = _trace_wide(e, prims, ranks, o, d)
+        assert got[1] == brute[1] and got[0].view(np.uint32) == np.float32(brute[0]).view(np.uint32), (i, got, brute)
+        n_hit += got[1] >= 0
+    assert n_hit > 100
+
+
+def test_sbvh_option_errors(host_scene):
+    with pytest.raises(RuntimeError):
+        host_scene.export("rebuilt", width=2, spatial_splits=True)
+    with pytest.raises(RuntimeError):
+        host_scene.export("rebuilt", width=4, spatial_splits=True, spatial_alpha=2.0)

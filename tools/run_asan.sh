@@ -1,0 +1,31 @@
+#!/bin/bash
+# The host-side code under AddressSanitizer + UndefinedBehaviorSanitizer: builds libcrt_host.so and the
+# oracle with -fsanitize=address,undefined (`make asan` in both directories), then runs the CPU tests that drive them
+# with the sanitizer runtimes preloaded into python.  Host code only: GPU sanitizers are not available on this pool.
+#   tools/run_asan.sh [LOG]        (default profiles/asan/run.log)
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+LOG=${1:-$R/profiles/asan/run.log}
+mkdir -p "$(dirname "$LOG")"
+make -C "$R/raytracer-cuda_amd" -j8 lib/libcrt_hip.so asan > /dev/null
+make -C "$R/oracle" asan > /dev/null
+ASAN_RT=$(gcc -print-file-name=libasan.so)
+UBSAN_RT=$(gcc -print-file-name=libubsan.so)
+export CRT_HOST_LIB=$R/raytracer-cuda_amd/lib_asan/libcrt_host.so
+export ORACLE_LIB=$R/oracle/_asan/liboracle.so
+# leaks: python itself holds its allocations at exit; odr: libstdc++ symbols seen twice through the preload
+export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=1:detect_odr_violation=0
+export UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1
+TESTS="tests/test_loader_fuzz.py tests/test_host_parity.py tests/test_image_io.py tests/test_camera_controller.py
+       tests/test_oracle.py tests/test_primitives_kat.py"
+cd "$R"
+{
+  echo "# tools/run_asan.sh at $(git rev-parse --short HEAD) ($(date -u +%FT%TZ))"
+  echo "# $CRT_HOST_LIB, $ORACLE_LIB; preload $ASAN_RT $UBSAN_RT"
+} > "$LOG"
+set +e
+LD_PRELOAD="$ASAN_RT $UBSAN_RT" python -u -m pytest $TESTS -v -p no:cacheprovider -m "not gpu" >> "$LOG" 2>&1
+rc=$?
+echo "# exit status $rc" >> "$LOG"
+tail -4 "$LOG"
+exit $rc
