@@ -83,9 +83,12 @@ def parse():
     ap.add_argument("--no-count", action="store_true", help="skip the work-counting launch (roofline -> null)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--cpu-single-seconds", type=float, default=8.0,
+                    help="cpu_baseline: also time one thread on a band of the frame for about this long (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="CPU-baseline threads (0 = min(16, usable cores), the GPU box's CPU share; 1 = the "
-                         "single-thread reference path of BASELINE.json configs[0])")
+                    help="CPU-baseline threads (0 = every usable core: the affinity set capped by the cgroup CPU "
+                         "quota, 16 of 256 CPUs on the GPU box; 1 = the single-thread reference path of BASELINE.json "
+                         "configs[0])")
     ap.add_argument("--save-ppm", default="", help="rank 0 writes the resolved frame here")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--kernel-variant", type=int, default=None, help="render-kernel variant (default: library's)")
@@ -114,6 +117,15 @@ def parse():
     return ap.parse_args()
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup may use (cgroup v2 cpu.max, e.g. "1600000 100000" = 16), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -133,10 +145,14 @@ def cpu_baseline(args, cam_floats, log_fn):
     import pyoracle
     from crt_amd import assets
     try:
-        ncpu = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        ncpu = os.cpu_count() or 1
-    threads = args.cpu_threads if args.cpu_threads > 0 else max(1, min(16, ncpu))
+        affinity = os.cpu_count() or 1
+    quota = cgroup_cpu_quota()
+    # usable cores: the affinity set, capped by the cgroup CPU quota (the GPU box: 256 CPUs in the affinity set, a
+    # 16-CPU quota; more threads than the quota only time-slice the same 16 CPUs)
+    ncpu = max(1, min(affinity, int(quota))) if quota else affinity
+    threads = args.cpu_threads if args.cpu_threads > 0 else ncpu
     sc = pyoracle.OracleScene(objload.load_scene(assets.scene_files(args.scene)))
     w, h = args.width, args.height
     t = time.perf_counter()
@@ -161,10 +177,24 @@ def cpu_baseline(args, cam_floats, log_fn):
         spp = nxt
     full = spp == args.spp
     log_fn(f"[cpu] oracle {w}x{h} {spp}spp: {c['rays']} rays in {dt:.2f}s on {threads} threads")
-    return {"value": round(c["rays"] / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+    rate = c["rays"] / dt
+    legs = [{"threads": threads, "Mrays_s": round(rate / 1e6, 3), "rays": c["rays"], "seconds": round(dt, 2),
+             "sample": f"full {w}x{h} frame, {spp} spp/pixel"}]
+    if threads > 1 and args.cpu_single_seconds > 0:
+        # one core, the same workload on a band of rows sized to about cpu_single_seconds at the per-thread rate
+        rows = int(max(1, min(h, round(args.cpu_single_seconds * rate / threads / max(c["rays"] / h, 1.0)))))
+        y0 = (h - rows) // 2
+        t = time.perf_counter()
+        _, _, c1t = sc.render(cam_floats, w, h, spp, args.bounces, seed=args.seed, nthreads=1, rect=(0, y0, w, y0 + rows))
+        d1 = time.perf_counter() - t
+        legs.append({"threads": 1, "Mrays_s": round(c1t["rays"] / d1 / 1e6, 3), "rays": c1t["rays"],
+                     "seconds": round(d1, 2), "sample": f"rows {y0}..{y0 + rows - 1} of the same frame, {spp} spp/pixel"})
+        log_fn(f"[cpu] oracle 1 thread: {c1t['rays']} rays in {d1:.2f}s")
+    return {"value": round(rate / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "what": "oracle/crt_oracle.c: C restatement of the reference's render path (bit-identical to the GPU "
                     "reference-BVH frames); the reference itself needs CUDA/cuRAND/SFML and cannot be built here",
-            "cpu_model": cpu_model(), "usable_cores": ncpu,
+            "cpu_model": cpu_model(), "usable_cores": ncpu, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "legs": legs,
             "sample": (f"the whole workload: {w}x{h}, {spp} spp/pixel, {args.bounces} bounces, seed {args.seed}" if full
                        else f"full {w}x{h} frame at {spp} of {args.spp} spp/pixel, {args.bounces} bounces, seed "
                             f"{args.seed}") + f" (same scene + camera as the GPU run; {c['rays']} rays in {dt:.2f} s)",
