@@ -1,0 +1,87 @@
+"""The spp-sharded multi-GPU path with the real HIP kernel (crt_amd/dist.py), 2 and 3 ranks.
+
+No 8-GPU node is available to this build, so the ranks share cuda:0 over the gloo backend (RCCL refuses two ranks on
+one GPU).  Everything else is the production path: each rank's kernel writes its shard's fp32 sums into a torch
+tensor, `reduce` / `all_reduce` sums them, rank 0 resolves with 1/spp_total.  Checked against the same shards rendered
+one after another in this process and summed on the host: with 2 ranks bit for bit (fp32 a + b is commutative); with 3
+to within one rounding of the sum order.  The resolved RGBA8 is writeColor of the reduced sums.
+"""
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import crt_amd
+from crt_amd import assets
+from crt_amd.dist import shard_spp, subsequence_base
+
+pytestmark = pytest.mark.gpu
+REPO = Path(__file__).resolve().parents[1]
+W, H, SPP = 160, 90, 24
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(tmp_path, world, reduce_op):
+    out = str(tmp_path / f"frame_{world}_{reduce_op}")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", str(REPO / "tests" / "helpers" / "dist_frame_worker.py"),
+           out, str(W), str(H), str(SPP), reduce_op]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert p.returncode == 0, p.stderr[-4000:]
+    return out
+
+
+def _shards(world):
+    hs = crt_amd.HostScene(assets.scene_files("cornell_bunny"))
+    sc = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
+    r = crt_amd.Renderer(W, H, 0)
+    r.set_camera(crt_amd.camera(SPP))
+    parts = []
+    for g in range(world):
+        r.init_rand(41, subsequence_base(g, W, H))
+        r.render(sc, shard_spp(SPP, world, g), 20)
+        r.synchronize()
+        parts.append(r.linear())
+    return parts, r
+
+
+@pytest.mark.parametrize("reduce_op", ["reduce", "all_reduce"])
+def test_two_ranks_equal_the_summed_shards(tmp_path, reduce_op):
+    out = _run(tmp_path, 2, reduce_op)
+    got = np.load(out + ".rank0.npz")
+    (a, b), r = _shards(2)
+    want = (a + b).astype(np.float32)
+    assert np.array_equal(got["lin"].view(np.uint32), want.view(np.uint32))
+    r.write_linear(want)
+    r.resolve(crt_amd.pixel_sample_scale(SPP))
+    r.synchronize()
+    assert np.array_equal(got["rgba"], r.rgba8())
+    if reduce_op == "all_reduce":
+        other = np.load(out + ".rank1.npz")
+        assert np.array_equal(other["lin"].view(np.uint32), want.view(np.uint32))
+
+
+def test_three_ranks_uneven_spp(tmp_path):
+    """24 spp over 3 ranks (8 each) and the remainder rule; the 3-term fp32 sum order is gloo's, so the check is one
+    rounding of the sum, and the frame is the 1-GPU estimator with different samples (statistical, not bitwise)."""
+    out = _run(tmp_path, 3, "reduce")
+    got = np.load(out + ".rank0.npz")["lin"]
+    parts, _ = _shards(3)
+    want = (parts[0] + parts[1]) + parts[2]
+    assert np.allclose(got, want, rtol=2 ** -22, atol=0)
+    one, _ = _shards(1)
+    # same estimator, independent samples: the frame means agree to Monte-Carlo noise (14,400 pixels x 24 samples)
+    m3 = got.reshape(-1, 3).astype(np.float64).mean(0)
+    m1 = one[0].reshape(-1, 3).astype(np.float64).mean(0)
+    assert (np.abs(m3 - m1) <= 0.03 * m1).all(), (m3 / SPP, m1 / SPP)
