@@ -47,6 +47,13 @@ def test_libraries_load_without_gpu():
     _lib.host()
 
 
+def test_timings_need_a_render():
+    from crt_amd import _lib
+    ms = (C.c_float * 3)()
+    assert _lib.hip().crt_renderer_last_timings(None, ms) == -1
+    assert _lib.hip().crt_build_flags() == 0
+
+
 def test_errors_are_reported_not_thrown():
     import crt_amd
     from crt_amd import _lib

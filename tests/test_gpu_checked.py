@@ -99,3 +99,21 @@ def test_variant8_probe_schedule_against_oracle(oracle_scenes, device_scenes):
     assert eq >= 0.999, f"only {eq:.6f} of pixels bit-identical"
     rays = r.counters()["rays"]
     assert abs(rays - o_cnt["rays"]) <= 1e-5 * o_cnt["rays"]
+
+
+def test_render_phase_timings(device_scenes):
+    """crt_renderer_last_timings: the whole render = probe + tile sort + main kernel (HIP events, ms)."""
+    hs, _ = device_scenes["cornell_bunny"]
+    sc = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
+    r = crt_amd.Renderer(160, 90)
+    r.set_camera(crt_amd.camera(64))
+    r.init_rand(41)
+    r.render(sc, 64, 20)                       # variant 8 with the cost probe
+    t = r.last_timings()
+    assert t["probe_sort_ms"] > 0 and t["main_kernel_ms"] > 0
+    assert abs(t["render_ms"] - (t["probe_sort_ms"] + t["main_kernel_ms"])) < 0.05 * t["render_ms"] + 0.05
+    assert abs(t["render_ms"] - r.last_kernel_ms()) < 1e-3
+    r.set_kernel_variant(4)
+    r.render(sc, 8, 20)                        # no probe: the main kernel is the whole render
+    t = r.last_timings()
+    assert t["probe_sort_ms"] < 0.05 and abs(t["render_ms"] - t["main_kernel_ms"]) < 0.05
