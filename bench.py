@@ -91,6 +91,9 @@ def parse():
                          "configs[0])")
     ap.add_argument("--save-ppm", default="", help="rank 0 writes the resolved frame here")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--shard", default="spp", choices=["spp", "pixels"],
+                    help="N > 1: spp sharding (the north star, default) or pixel sharding (every N-th tile with all "
+                         "samples: the 1-GPU frame bit for bit, but bounded by the slowest tile's sample chain)")
     ap.add_argument("--kernel-variant", type=int, default=None, help="render-kernel variant (default: library's)")
     ap.add_argument("--regen-threshold", type=int, default=None,
                     help="parked lanes before a regeneration pass (default: the library's, 44 for 4-wide scenes)")
@@ -339,7 +342,7 @@ def main():
     if args.critical_tiles is not None:
         r.set_critical_tiles(args.critical_tiles, args.critical_lanes)
     r.set_camera(cam)
-    fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world)
+    fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard)
     log_r(f"[plan] {world} rank(s), spp per rank {[fr.spp] if world == 1 else 'spp/N'}")
 
     for i in range(args.warmup):
@@ -459,7 +462,7 @@ def main():
             "config": {"workload": workload_name(args),
                        "width": W, "height": H, "spp": args.spp, "max_bounces": args.bounces, "seed": args.seed,
                        "triangles": counts["n_indices"] // 3, "bvh": bvh_desc, "kernel_variant": variant,
-                       "parallelism": f"spp-shard x{world}" + ((" + RCCL reduce of fp32 framebuffer" if args.dist_backend == "nccl"
+                       "parallelism": f"{args.shard}-shard x{world}" + ((" + RCCL reduce of fp32 framebuffer" if args.dist_backend == "nccl"
                                                                   else f" + {args.dist_backend} reduce (rehearsal)")
                                                                  if world > 1 else "")},
             "frame_wall_s": round(ms_per_step / 1e3, 4),

@@ -261,6 +261,12 @@ int  crt_renderer_set_regen_threshold(crt_renderer* r, int lanes);
  * regeneration threshold.  A frame with few tiles per wave slot ends with its most expensive tile, whose pixels' sample
  * chains are sequential; waiting less for the wave's other lanes shortens that chain.  Results never depend on it. */
 int  crt_renderer_set_critical_tiles(crt_renderer* r, int tiles, int lanes);
+/* Pixel sharding, the bit-exact multi-GPU mode: renders of this renderer draw only shard `shard` of
+ * `shards` -- every shards-th 8x8 tile of the cost order (or of row order without the probe) -- with all samples, and
+ * leave every other pixel of the linear framebuffer at 0.  Summing the shards' framebuffers (the same reduce as spp
+ * sharding, every rank with subsequence base 0) gives the unsharded frame bit for bit.  4-wide rebuilt scenes only
+ * (variant 8); no CRT_RENDER_ACCUMULATE.  (0, 1) = unsharded, the default. */
+int  crt_renderer_set_pixel_shard(crt_renderer* r, int shard, int shards);
 /* Variant 4: per-lane traversal-stack entries kept in LDS (1..16, default 16); deeper entries spill to a
  * per-pixel region in HBM.  Results do not depend on it (tests force the HBM path with 1). */
 int  crt_renderer_set_stack_lds(crt_renderer* r, int entries);

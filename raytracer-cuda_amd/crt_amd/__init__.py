@@ -227,6 +227,11 @@ class Renderer:
     def set_critical_tiles(self, tiles: int = -1, lanes: int = 16):
         check(_lib.hip().crt_renderer_set_critical_tiles(self.h, int(tiles), int(lanes)), "set_critical_tiles")
 
+    def set_pixel_shard(self, shard: int = 0, shards: int = 1):
+        """Render only every shards-th 8x8 tile (from shard) with all samples; other pixels stay 0 (bit-exact
+        multi-GPU mode, crt_renderer_set_pixel_shard)."""
+        check(_lib.hip().crt_renderer_set_pixel_shard(self.h, int(shard), int(shards)), "set_pixel_shard")
+
     def set_kernel_variant(self, variant: int):
         check(_lib.hip().crt_renderer_set_kernel_variant(self.h, int(variant)), "set_kernel_variant")
 

@@ -106,7 +106,7 @@ HIP_SYMBOLS = [
     "crt_renderer_last_kernel_name", "crt_renderer_last_timings",
     "crt_renderer_attach_linear", "crt_renderer_set_kernel_variant", "crt_renderer_get_schedule_stats",
     "crt_renderer_set_regen_threshold", "crt_renderer_set_occupancy_target",
-    "crt_build_mesh_bvh", "crt_renderer_set_schedule", "crt_renderer_set_critical_tiles",
+    "crt_build_mesh_bvh", "crt_renderer_set_schedule", "crt_renderer_set_critical_tiles", "crt_renderer_set_pixel_shard",
     "crt_selftest_math", "crt_selftest_rng", "crt_selftest_geometry", "crt_selftest_scan", "crt_selftest_rcp",
     "crt_selftest_uv_div", "crt_selftest_sqrt",
 ]
@@ -159,6 +159,7 @@ def hip():
             "crt_renderer_init_rand": ([P, u64, u64, P], i32), "crt_renderer_set_camera": ([P, P], i32),
             "crt_renderer_render": ([P, P, i32, i32, C.c_uint, P], i32),
             "crt_renderer_resolve": ([P, f32, P], i32), "crt_renderer_render_frame": ([P, P, P], i32),
+            "crt_renderer_set_pixel_shard": ([P, i32, i32], i32),
             "crt_renderer_synchronize": ([P, P], i32), "crt_renderer_last_timings": ([P, P], i32),
             "crt_renderer_read_linear": ([P, P], i32), "crt_renderer_read_rgba8": ([P, P], i32),
             "crt_renderer_read_rng": ([P, P], i32), "crt_renderer_write_linear": ([P, P], i32),

@@ -44,10 +44,20 @@ class ShardedFrameRenderer:
     writes directly (crt_renderer_attach_linear); the kernel, the collective and the
     resolve are all enqueued on torch's current stream, so no host sync sits between
     them.  `reduce_op` is "all_reduce" (every rank holds the frame) or "reduce" (rank 0).
+
+    `mode` "spp" (default, the north star): rank g renders spp_g samples of every pixel from subsequence family
+    pixel + g*W*H; N > 1 is the same estimator with other samples.  "pixels" (SURVEY §8e's bit-exact alternative):
+    rank g renders every N-th 8x8 tile of the cost order with ALL samples from the unsharded RNG streams and leaves the
+    other pixels 0 (crt_renderer_set_pixel_shard), so the same reduce yields the 1-GPU frame bit for bit.  Its speed-up
+    is bounded by the slowest tile's sequential sample chain, so it is the parity mode, not the bench's.
     """
 
     def __init__(self, renderer, scene, spp_total: int, max_bounces: int = 20, seed: int = 41,
-                 rank: int = 0, world: int = 1, group=None, reduce_op: str = "reduce", fb_device=None):
+                 rank: int = 0, world: int = 1, group=None, reduce_op: str = "reduce", fb_device=None,
+                 mode: str = "spp"):
+        if mode not in ("spp", "pixels"):
+            raise ValueError("mode must be 'spp' or 'pixels'")
+        self.mode = mode
         import torch
         self.torch = torch
         self.r = renderer
@@ -57,8 +67,13 @@ class ShardedFrameRenderer:
         self.seed = int(seed)
         self.rank, self.world, self.group = rank, world, group
         self.reduce_op = reduce_op
-        self.spp = shard_spp(spp_total, world, rank)
-        self.subseq = subsequence_base(rank, renderer.width, renderer.height)
+        if mode == "spp":
+            self.spp = shard_spp(spp_total, world, rank)
+            self.subseq = subsequence_base(rank, renderer.width, renderer.height)
+        else:
+            self.spp = int(spp_total)
+            self.subseq = 0
+            renderer.set_pixel_shard(rank, world)
         self.fb_device = fb_device or f"cuda:{renderer.device}"
         self.fb = torch.zeros((renderer.height, renderer.width, 3), dtype=torch.float32, device=self.fb_device)
         renderer.attach_linear(self.fb.data_ptr())

@@ -77,6 +77,8 @@ struct RenderParams {
     uint32_t* __restrict__ probe_cost;    // probe launch (variant 4): rays per pixel; nothing else is written
     int crit_tiles, crit_threshold;       // variant 8: the first crit_tiles tiles of the cost order regenerate at
                                           // crit_threshold parked lanes instead of regen_threshold
+    int tile_shard, tile_shards;          // variant 8, pixel sharding: this launch renders the tiles t with
+                                          // t % tile_shards == tile_shard (the cost order holds them first)
 };
 
 #ifdef CRT_PROFILE_PAIRS
@@ -1233,8 +1235,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: LDS bases stay scalar
     int x, y;
-    if (TILED) {                               // workgroup b renders 8x8 tile order[b]
-        const uint32_t t = P.order ? P.order[blockIdx.x] : blockIdx.x;
+    if (TILED) {                               // workgroup b renders 8x8 tile order[b]; without an order, tile b
+                                               // (pixel shards: tile b * tile_shards + tile_shard)
+        const uint32_t t = P.order ? P.order[blockIdx.x] : blockIdx.x * (uint32_t)P.tile_shards + (uint32_t)P.tile_shard;
         x = (int)(t % (uint32_t)P.tiles_x) * 8 + (lane & 7);
         y = (int)(t / (uint32_t)P.tiles_x) * 8 + (lane >> 3);
     } else {
@@ -1919,6 +1922,15 @@ __global__ void crt_tile_neighbour_kernel(const uint32_t* __restrict__ key_in, i
 
 // No probe: 8x8 tiles in row order, pixels row-major inside a tile (a wave's first 64 slots are one tile, so
 // its primary rays are coherent); slots of partial edge tiles hold ~0.
+// Pixel sharding (crt_renderer_set_pixel_shard): the tiles of other shards get key 0 and this shard's keys + 1, so
+// the descending cost order puts exactly this shard's tiles first, whatever order the counting sort gives equal keys.
+__global__ void crt_tile_shard_mask_kernel(uint32_t* __restrict__ key, int n_tiles, int shard, int shards) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_tiles) return;
+    const uint32_t k = key[t];
+    key[t] = t % shards == shard ? (k < 0xffffffffu ? k + 1u : k) : 0u;
+}
+
 __global__ void crt_order_tiles_kernel(uint32_t* __restrict__ order, int width, int height, int n_slots) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_slots) return;
@@ -2431,6 +2443,7 @@ struct crt_renderer {
     int regen_threshold = 24;      // variants 2/3
     int regen_threshold_wide = 44; // variants 4/7/8 (measured: 40 for variant 4, profiles/r01d; 44-48 for 8, r01af)
     int crit_tiles = -1;           // variant 8: leading tiles of the cost order regenerating at crit_threshold; -1 = 4 per CU
+    int tile_shard = 0, tile_shards = 1;   // pixel sharding (crt_renderer_set_pixel_shard)
     int crit_threshold = 16;       // (measured: profiles/r02h, r02i)
     int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 6 for 4-wide scenes, 5 otherwise
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
@@ -2850,6 +2863,15 @@ int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int f
     return CRT_OK;
 }
 
+int crt_renderer_set_pixel_shard(crt_renderer* R, int shard, int shards) {
+    if (!R || shards < 1 || shard < 0 || shard >= shards) return set_error(CRT_ERR_INVALID_ARGUMENT, "shard in [0, shards)");
+    const int n_tiles = ((R->width + 7) / 8) * ((R->height + 7) / 8);
+    if (shards > n_tiles) return set_error(CRT_ERR_INVALID_ARGUMENT, "more shards than 8x8 tiles");
+    R->tile_shard = shard;
+    R->tile_shards = shards;
+    return CRT_OK;
+}
+
 int crt_renderer_set_critical_tiles(crt_renderer* R, int tiles, int lanes) {
     if (!R || tiles < -1 || lanes < 1 || lanes > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "critical tiles >= -1, lanes 1..64");
     R->crit_tiles = tiles;
@@ -2912,6 +2934,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.rcp_w = R->rcp_w; P.rcp_h = R->rcp_h; P.fast_uv = R->fast_uv;
     P.ovf = nullptr;
     P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0; P.crit_tiles = 0; P.crit_threshold = 64;
+    P.tile_shard = 0; P.tile_shards = 1;
     P.stack_cap = S->stack_cap;
     P.sphere_first = S->sphere_first;
     P.n_ray_spheres = S->n_ray_spheres;
@@ -2954,6 +2977,14 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     // pixel queue) for short renders such as the 1-spp interactive frames
     int wv = R->variant;
     if (S->width == 4 && wv != 4 && wv != 7 && wv != 8) wv = probe_spp_for(R, spp) > 0 ? 8 : 7;
+    if (R->tile_shards > 1) {
+        // pixel sharding: variant 8 renders this shard's tiles; every other pixel of the framebuffer is 0, so the sum
+        // of the shards' framebuffers (one collective) is the unsharded frame exactly (x + 0 = x)
+        if (S->width != 4) return set_error(CRT_ERR_UNSUPPORTED, "pixel sharding needs a 4-wide rebuilt scene (variant 8)");
+        if (P.accumulate) return set_error(CRT_ERR_INVALID_ARGUMENT, "pixel sharding does not accumulate");
+        wv = 8;
+        HIP_TRY(hipMemsetAsync(R->d_sum, 0, (size_t)R->width * R->height * 3 * sizeof(float), st));
+    }
     if (S->width == 4 && wv == 8) {
         const size_t n_pix = (size_t)R->width * R->height;
         const int tiles_x = (R->width + 7) / 8, n_tiles = tiles_x * ((R->height + 7) / 8);
@@ -2985,6 +3016,9 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
                                    R->d_tile_key, tiles_x, n_tiles, R->d_tile_cost);
                 HIP_TRY(hipMemcpyAsync(R->d_tile_key, R->d_tile_cost, (size_t)n_tiles * 4, hipMemcpyDeviceToDevice, st));
             }
+            if (R->tile_shards > 1)
+                hipLaunchKernelGGL(crt_tile_shard_mask_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st,
+                                   R->d_tile_key, n_tiles, R->tile_shard, R->tile_shards);
             const unsigned ob = (unsigned)((n_tiles + ORDER_ITEMS - 1) / ORDER_ITEMS);
             HIP_TRY(hipMemsetAsync(R->d_order_hist, 0, ORDER_KEYS * 4, st));
             hipLaunchKernelGGL(crt_order_hist_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key, n_tiles, R->d_order_hist);
@@ -2995,7 +3029,10 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             P.crit_tiles = R->crit_tiles < 0 ? 4 * R->n_cus : R->crit_tiles;
             P.crit_threshold = R->crit_threshold;
         }
-        const dim3 tgrid(n_tiles), tblock(64);
+        P.tile_shard = R->tile_shard;
+        P.tile_shards = R->tile_shards;
+        if (P.crit_tiles > 0) P.crit_tiles = (P.crit_tiles + R->tile_shards - 1) / R->tile_shards;
+        const dim3 tgrid((unsigned)((n_tiles - R->tile_shard + R->tile_shards - 1) / R->tile_shards)), tblock(64);
         const char* cs = cnt ? "true" : "false";
         HIP_TRY(hipEventRecord(R->ev_main, st));
         if (occ >= 7) {

@@ -16,6 +16,7 @@ from crt_amd import assets  # noqa: E402
 from crt_amd.dist import ShardedFrameRenderer, dist_env  # noqa: E402
 
 out, w, h, spp, reduce_op = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
+mode = sys.argv[6] if len(sys.argv) > 6 else "spp"
 rank, local, world = dist_env()
 torch.cuda.set_device(0)
 dist.init_process_group("gloo")
@@ -23,11 +24,12 @@ hs = crt_amd.HostScene(assets.scene_files("cornell_bunny"))
 sc = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
 r = crt_amd.Renderer(w, h, 0)
 r.set_camera(crt_amd.camera(spp))
-fr = ShardedFrameRenderer(r, sc, spp, 20, 41, rank, world, reduce_op=reduce_op)
+fr = ShardedFrameRenderer(r, sc, spp, 20, 41, rank, world, reduce_op=reduce_op, mode=mode)
 fr.render()
 torch.cuda.synchronize()
 lin = fr.linear()
 if rank == 0 or reduce_op == "all_reduce":
-    np.savez(f"{out}.rank{rank}.npz", lin=lin, rgba=r.rgba8(), spp=fr.spp, subseq=fr.subseq)
+    np.savez(f"{out}.rank{rank}.npz", lin=lin, rgba=r.rgba8(), spp=fr.spp, subseq=fr.subseq,
+             rays=r.counters()["rays"])
 dist.barrier()
 dist.destroy_process_group()

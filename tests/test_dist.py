@@ -37,8 +37,13 @@ class OracleShardRenderer:
         self.ptr = None
         self.resolved = None
 
+    shard, shards = 0, 1
+
     def attach_linear(self, ptr):
         self.ptr = ptr
+
+    def set_pixel_shard(self, shard, shards):
+        self.shard, self.shards = shard, shards
 
     def init_rand(self, seed, subseq, stream=None):
         self.seed, self.subseq = seed, subseq
@@ -46,20 +51,25 @@ class OracleShardRenderer:
     def render(self, scene, spp, bounces, stream=None):
         s, _, _ = self.o.render(self.cam, self.width, self.height, spp, bounces, seed=self.seed,
                                 subseq_base=self.subseq, nthreads=2)
+        if self.shards > 1:   # crt_renderer_set_pixel_shard without the probe: every shards-th 8x8 tile in row order
+            tx = (self.width + 7) // 8
+            for t in range(tx * ((self.height + 7) // 8)):
+                if t % self.shards != self.shard:
+                    s[(t // tx) * 8:(t // tx) * 8 + 8, (t % tx) * 8:(t % tx) * 8 + 8] = 0
         C.memmove(self.ptr, s.ctypes.data, s.nbytes)
 
     def resolve(self, scale, stream=None):
         self.resolved = scale
 
 
-def _worker(rank, world, port, files, q, reduce_op="all_reduce"):
+def _worker(rank, world, port, files, q, reduce_op="all_reduce", mode="spp"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import objload
     import pyoracle
     o = pyoracle.OracleScene(objload.load_scene(files))
     r = OracleShardRenderer(o, pyoracle.camera(), W, H)
-    fr = ShardedFrameRenderer(r, None, SPP, 20, 41, rank, world, reduce_op=reduce_op, fb_device="cpu")
+    fr = ShardedFrameRenderer(r, None, SPP, 20, 41, rank, world, reduce_op=reduce_op, fb_device="cpu", mode=mode)
     fr.render()
     q.put((rank, fr.spp, fr.subseq, fr.linear(), r.resolved))
     dist.destroy_process_group()
@@ -126,3 +136,32 @@ def test_gloo_reduce_to_rank0(scenes, world):
     assert np.allclose(res[0][3], ref, rtol=0, atol=1e-5)
     assert res[0][4] == np.float32(1) / np.float32(SPP)          # rank 0: writeColor scale of the whole frame
     assert all(r[4] is None for r in res[1:])                    # non-root ranks: no resolve
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_pixel_shards_equal_the_unsharded_frame(scenes, world):
+    """mode="pixels" (SURVEY §8e's bit-exact alternative): every rank renders its tiles with all samples from the
+    unsharded RNG streams and zeros elsewhere, so the reduced frame IS the 1-GPU frame, bit for bit."""
+    import objload
+    import pyoracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, scenes["cornell"], q, "reduce", "pixels"))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in ps], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [SPP] * world and [r[2] for r in res] == [0] * world
+    o = pyoracle.OracleScene(objload.load_scene(scenes["cornell"]))
+    full = o.render(pyoracle.camera(), W, H, SPP, 20)[0]
+    assert np.array_equal(res[0][3].view(np.uint32), full.view(np.uint32))
+    assert res[0][4] == np.float32(1) / np.float32(SPP)
+
+
+def test_pixel_mode_argument_checks():
+    with pytest.raises(ValueError):
+        ShardedFrameRenderer(None, None, 8, mode="rows")

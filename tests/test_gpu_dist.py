@@ -32,11 +32,11 @@ def _port():
     return p
 
 
-def _run(tmp_path, world, reduce_op):
-    out = str(tmp_path / f"frame_{world}_{reduce_op}")
+def _run(tmp_path, world, reduce_op, spp=SPP, mode="spp"):
+    out = str(tmp_path / f"frame_{world}_{reduce_op}_{mode}")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", str(REPO / "tests" / "helpers" / "dist_frame_worker.py"),
-           out, str(W), str(H), str(SPP), reduce_op]
+           out, str(W), str(H), str(spp), reduce_op, mode]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="2"))
     assert p.returncode == 0, p.stderr[-4000:]
     return out
@@ -85,3 +85,50 @@ def test_three_ranks_uneven_spp(tmp_path):
     m3 = got.reshape(-1, 3).astype(np.float64).mean(0)
     m1 = one[0].reshape(-1, 3).astype(np.float64).mean(0)
     assert (np.abs(m3 - m1) <= 0.03 * m1).all(), (m3 / SPP, m1 / SPP)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pixel_shards_equal_the_one_gpu_frame(tmp_path, world):
+    """mode="pixels": every rank renders every world-th tile of the cost order (64 spp: the probe and the tile sort run)
+    with all samples, zeros elsewhere; the reduced frame, its RGBA8 and the summed ray count equal the 1-GPU frame's
+    bit for bit (SURVEY §8e's bit-exact multi-GPU mode)."""
+    spp = 64
+    out = _run(tmp_path, world, "reduce", spp=spp, mode="pixels")
+    got = np.load(out + ".rank0.npz")
+    hs = crt_amd.HostScene(assets.scene_files("cornell_bunny"))
+    sc = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
+    r = crt_amd.Renderer(W, H, 0)
+    r.set_camera(crt_amd.camera(spp))
+    r.init_rand(41)
+    r.render(sc, spp, 20)
+    r.resolve(crt_amd.pixel_sample_scale(spp))
+    r.synchronize()
+    assert r.last_kernel_name() == "crt_render_kernel<false, 8, 6>"
+    assert np.array_equal(got["lin"].view(np.uint32), r.linear().view(np.uint32))
+    assert np.array_equal(got["rgba"], r.rgba8())
+
+
+def test_pixel_shard_rays_add_up(device_scenes):
+    """In one process: the shards' ray counts sum to the unsharded frame's, and each shard leaves the other tiles 0."""
+    hs, _ = device_scenes["cornell_bunny"]
+    sc = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
+    r = crt_amd.Renderer(W, H, 0)
+    r.set_camera(crt_amd.camera(64))
+    r.init_rand(41)
+    r.render(sc, 64, 20)
+    r.synchronize()
+    full, rays = r.linear(), r.counters()["rays"]
+    acc, tot = np.zeros_like(full), 0
+    for g in range(3):
+        r.set_pixel_shard(g, 3)
+        r.init_rand(41)
+        r.render(sc, 64, 20)
+        r.synchronize()
+        part = r.linear()
+        assert (part != 0).any(axis=-1).mean() < 0.5
+        acc += part
+        tot += r.counters()["rays"]
+    assert np.array_equal(acc.view(np.uint32), full.view(np.uint32)) and tot == rays
+    with pytest.raises(crt_amd.CrtError):
+        r.render(sc, 64, 20, accumulate=True)
+    r.set_pixel_shard(0, 1)
