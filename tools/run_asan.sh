@@ -27,5 +27,14 @@ set +e
 LD_PRELOAD="$ASAN_RT $UBSAN_RT" python -u -m pytest $TESTS -v -p no:cacheprovider -m "not gpu" >> "$LOG" 2>&1
 rc=$?
 echo "# exit status $rc" >> "$LOG"
+# phase 2: the HIP library's host half, built by hipcc with clang's sanitizers (its own runtime, so a separate process);
+# the plain host library and oracle
+CLANG_RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
+echo "# phase 2: CRT_HIP_LIB=$R/raytracer-cuda_amd/lib_asan/libcrt_hip.so, preload $CLANG_RT" >> "$LOG"
+CRT_HIP_LIB=$R/raytracer-cuda_amd/lib_asan/libcrt_hip.so CRT_HOST_LIB= ORACLE_LIB= LD_PRELOAD="$CLANG_RT" \
+    python -u -m pytest tests/test_rebuilt_bvh.py tests/test_loader_fuzz.py tests/test_abi.py -v -p no:cacheprovider \
+    -m "not gpu" >> "$LOG" 2>&1
+rc2=$?
+echo "# exit status $rc2" >> "$LOG"
 tail -4 "$LOG"
-exit $rc
+[ $rc -eq 0 ] && [ $rc2 -eq 0 ]
