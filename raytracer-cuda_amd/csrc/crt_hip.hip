@@ -77,8 +77,6 @@ struct RenderParams {
     uint32_t* __restrict__ probe_cost;    // probe launch (variant 4): rays per pixel; nothing else is written
     int crit_tiles, crit_threshold;       // variant 8: the first crit_tiles tiles of the cost order regenerate at
                                           // crit_threshold parked lanes instead of regen_threshold
-    int tile_shard, tile_shards;          // variant 8, pixel sharding: this launch renders the tiles t with
-                                          // t % tile_shards == tile_shard (the cost order holds them first)
 };
 
 #ifdef CRT_PROFILE_PAIRS
@@ -1235,9 +1233,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: LDS bases stay scalar
     int x, y;
-    if (TILED) {                               // workgroup b renders 8x8 tile order[b]; without an order, tile b
-                                               // (pixel shards: tile b * tile_shards + tile_shard)
-        const uint32_t t = P.order ? P.order[blockIdx.x] : blockIdx.x * (uint32_t)P.tile_shards + (uint32_t)P.tile_shard;
+    if (TILED) {                               // workgroup b renders 8x8 tile order[b]
+        const uint32_t t = P.order ? P.order[blockIdx.x] : blockIdx.x;
         x = (int)(t % (uint32_t)P.tiles_x) * 8 + (lane & 7);
         y = (int)(t / (uint32_t)P.tiles_x) * 8 + (lane >> 3);
     } else {
@@ -1929,6 +1926,12 @@ __global__ void crt_tile_shard_mask_kernel(uint32_t* __restrict__ key, int n_til
     if (t >= n_tiles) return;
     const uint32_t k = key[t];
     key[t] = t % shards == shard ? (k < 0xffffffffu ? k + 1u : k) : 0u;
+}
+
+// Pixel sharding without the probe: slot k holds tile k * shards + shard.
+__global__ void crt_shard_tiles_kernel(uint32_t* __restrict__ order, int n_tiles, int shard, int shards) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k * shards + shard < n_tiles) order[k] = (uint32_t)(k * shards + shard);
 }
 
 __global__ void crt_order_tiles_kernel(uint32_t* __restrict__ order, int width, int height, int n_slots) {
@@ -2934,7 +2937,6 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.rcp_w = R->rcp_w; P.rcp_h = R->rcp_h; P.fast_uv = R->fast_uv;
     P.ovf = nullptr;
     P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0; P.crit_tiles = 0; P.crit_threshold = 64;
-    P.tile_shard = 0; P.tile_shards = 1;
     P.stack_cap = S->stack_cap;
     P.sphere_first = S->sphere_first;
     P.n_ray_spheres = S->n_ray_spheres;
@@ -3029,8 +3031,11 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             P.crit_tiles = R->crit_tiles < 0 ? 4 * R->n_cus : R->crit_tiles;
             P.crit_threshold = R->crit_threshold;
         }
-        P.tile_shard = R->tile_shard;
-        P.tile_shards = R->tile_shards;
+        if (R->tile_shards > 1 && !P.order) {   // pixel shard without the probe: this shard's tiles in row order
+            hipLaunchKernelGGL(crt_shard_tiles_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_order, n_tiles,
+                               R->tile_shard, R->tile_shards);
+            P.order = R->d_order;
+        }
         if (P.crit_tiles > 0) P.crit_tiles = (P.crit_tiles + R->tile_shards - 1) / R->tile_shards;
         const dim3 tgrid((unsigned)((n_tiles - R->tile_shard + R->tile_shards - 1) / R->tile_shards)), tblock(64);
         const char* cs = cnt ? "true" : "false";
