@@ -3,7 +3,7 @@
 // write it as PNG or binary PPM by extension (rows flipped like WindowManager::drawFrame's flipVertically).
 //
 //   crt_render [-w W] [-h H] [-spp N] [-seed S] [-o out.ppm] [-pos x y z] [-fov deg] [-bvh reference|rebuilt]
-//              [-leaf N] model.obj...
+//              [-leaf N] [-sbvh] model.obj...       (-sbvh: rebuilt tree with spatial splits)
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -38,6 +38,7 @@ int main(int argc, char** argv) {
             else if (a == "-pos") { need(3); for (float& p : pos) p = (float)std::atof(argv[++i]); }
             else if (a == "-bvh") { need(1); std::string m = argv[++i]; opts.bvh = m == "rebuilt" ? CRT_BVH_REBUILT : CRT_BVH_REFERENCE; }
             else if (a == "-leaf") { need(1); opts.leaf_size = std::atoi(argv[++i]); }
+            else if (a == "-sbvh") { opts.bvh = CRT_BVH_REBUILT; opts.spatial_splits = 1; }
             else files.push_back(a);
         }
         const float ASPECT_RATIO = 16.0f / 9.0f;                 // EntryPoint.cu:16-20
