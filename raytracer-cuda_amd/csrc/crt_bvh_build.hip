@@ -707,7 +707,7 @@ extern "C" int crt_build_mesh_bvh(int device, const float* positions, uint32_t v
 // ======================================================================================================
 // The CRT_BVH_REBUILT binned-SAH build (crt_sah.h's Builder) on the GPU, level by level.
 //
-// Same rules as the host builder: node box = padded (pad_box) bounds of its items; 32 bins per axis over
+// Same rules as the host builder: node box = padded (pad_box) bounds of its items; CRT_SAH_BINS bins per axis over
 // the centroid extent; SAH sweep with traversal cost C_trav and unit primitive cost; leaf when the node
 // may be a leaf (no spheres, count <= leaf_size) and splitting does not pay; count 1 is a leaf; no usable
 // split (all centroids equal) splits in half.  Bin counts and boxes are order-independent, so the splits
@@ -718,8 +718,8 @@ extern "C" int crt_build_mesh_bvh(int device, const float* positions, uint32_t v
 
 namespace {
 
-#ifndef CRT_SAH_BINS
-#define CRT_SAH_BINS 32
+#ifndef CRT_SAH_BINS   // set by crt_sah.h (128)
+#define CRT_SAH_BINS 128
 #endif
 constexpr int SAH_BINS = CRT_SAH_BINS;
 constexpr int SAH_RED = 13 + 3 * SAH_BINS * 7;   // box lo3 hi3, centroid lo3 hi3, spheres; bins: count lo3 hi3

@@ -4,7 +4,7 @@
 // ten triangles and unpadded leaf boxes; on the benchmark scenes every ray ends up testing ~26 triangles
 // and ~18 boxes.  The rebuilt mode keeps the reference's hit rule (closest t in [0.001, closest], ties
 // to the primitive with the higher reference DFS rank) but traverses a tree built for the hardware:
-//   * binned SAH (32 bins, all three axes) over primitive boxes, leaves of <= leaf_size triangles;
+//   * binned SAH (CRT_SAH_BINS = 128 bins, all three axes) over primitive boxes, leaves of <= leaf_size triangles;
 //   * every box padded outward (pad_box), so rounding in the slab test cannot cull a genuine hit;
 //   * emitted as threaded DFS arrays (same node format as the reference mode, crt_device.h), once per
 //     ray-direction class (dominant axis x sign): children ordered near-first along that axis, so the
@@ -68,8 +68,11 @@ public:
     int max_depth() const { return max_depth_; }
 
 private:
+// 128 bins (round 3, profiles/r03o: config C -0.2 %, config E -1.8 % against 32, three interleaved rounds each;
+// 64 bins made E 3.5 % slower, reproducibly).  A build-time knob shared with the GPU builder (crt_bvh_build.hip),
+// whose trees are tested identical to this builder's.
 #ifndef CRT_SAH_BINS
-#define CRT_SAH_BINS 32
+#define CRT_SAH_BINS 128
 #endif
     static constexpr int kBins = CRT_SAH_BINS;
     std::vector<Item> items_;
