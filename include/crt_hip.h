@@ -235,14 +235,15 @@ int  crt_renderer_init_rand(crt_renderer* r, unsigned long long seed, unsigned l
  * rebuilt tree's slab test needs |o| * 2^64 finite; every real scene is many orders of magnitude inside it). */
 int  crt_renderer_set_camera(crt_renderer* r, const crt_camera_desc* cam);
 /* Render-kernel variant (identical results, different wave scheduling).  Scenes with threaded binary nodes
- * (CRT_BVH_REFERENCE, or REBUILT width 2; default 3): 0 = per-lane BVH traversal with per-lane leaf loops; 1 = per-lane
+ * (CRT_BVH_REFERENCE, or REBUILT width 2): 0 = per-lane BVH traversal with per-lane leaf loops; 1 = per-lane
  * traversal with wave-cooperative leaf intersection; 2 = 1 + traversal-step scheduling with parked-lane regeneration
  * (lanes start their next ray without waiting for the wave's slowest trace); 3 = 2 + next-node prefetch overlapping
- * the leaf rounds; 4, 7, 8 run variant 3.  Scenes with 4-wide nodes (CRT_BVH_REBUILT, width 4): 4 = the variant-3
- * scheduling over 4-wide nodes with a per-lane stack, 16x16-pixel workgroups; 7 = 4 with a persistent grid whose lanes
- * take pixels from a global queue (no lane waits for its wave's slowest pixel); 8 = 4 with one wave per workgroup over
- * 8x8 tiles in cost-probe order (crt_renderer_set_schedule); anything else = automatic: 8 when the render runs the cost
- * probe (spp >= its minimum), else 7.  Accepted values: 0-4, 7, 8. */
+ * the leaf rounds; 10 = 3 with one wave per workgroup over 8x8 tiles in cost-probe order; anything else = automatic:
+ * 10 when the render runs the cost probe (spp >= its minimum), else 3.  Scenes with 4-wide nodes (CRT_BVH_REBUILT,
+ * width 4): 4 = the variant-3 scheduling over 4-wide nodes with a per-lane stack, 16x16-pixel workgroups; 7 = 4 with a
+ * persistent grid whose lanes take pixels from a global queue (no lane waits for its wave's slowest pixel); 8 = 4 with
+ * one wave per workgroup over 8x8 tiles in cost-probe order (crt_renderer_set_schedule); anything else = automatic: 8
+ * when the render runs the cost probe, else 7.  Accepted values: -1 (automatic, the default), 0-4, 7, 8, 10. */
 int  crt_renderer_set_kernel_variant(crt_renderer* r, int variant);
 /* Work order of variants 7 and 8 (4-wide scenes).  Cost probe: before the render, variant 4 traces probe_spp samples
  * per pixel over the same RNG state without writing anything, and the per-pixel work estimates order the work

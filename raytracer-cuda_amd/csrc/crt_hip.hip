@@ -1203,7 +1203,7 @@ __device__ unsigned long long g_wave_prof[2 * 4 * 65536];
 
 // Waves per workgroup: 4 (16x16 pixels), or 1 for variant 8 (one 8x8 tile per workgroup, so a finished wave frees
 // its slot at once instead of holding it until its three siblings end).
-template <int VARIANT> struct KernelShape { static constexpr int waves = VARIANT == 8 ? 1 : 4; };
+template <int VARIANT> struct KernelShape { static constexpr int waves = VARIANT == 8 || VARIANT == 10 ? 1 : 4; };
 
 template <bool COUNT, int VARIANT, int MINW>
 __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_render_kernel(RenderParams P) {
@@ -1215,6 +1215,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     // variant 4: 16 LDS stack entries per lane at 5 waves/SIMD; 12 at 6+ so 6 workgroups fit the 160 KiB
     constexpr bool PERSIST = VARIANT == 7;
     constexpr bool TILED = VARIANT == 8;    // variant 4 with one wave per workgroup and a tile order
+    constexpr bool TILES = TILED || VARIANT == 10;   // one 8x8 tile per one-wave workgroup (variant 10: variant 3's program)
     constexpr bool WIDE = VARIANT == 4 || PERSIST || TILED;
     constexpr int SD = WIDE ? (MINW >= 7 ? 11 : MINW >= 6 ? 12 : STACK_LDS) : 1;
     __shared__ uint32_t stack_lds[WIDE ? WGW * SD * 64 : 1];
@@ -1233,7 +1234,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: LDS bases stay scalar
     int x, y;
-    if (TILED) {                               // workgroup b renders 8x8 tile order[b]
+    if (TILES) {                               // workgroup b renders 8x8 tile order[b]
         const uint32_t t = P.order ? P.order[blockIdx.x] : blockIdx.x;
         x = (int)(t % (uint32_t)P.tiles_x) * 8 + (lane & 7);
         y = (int)(t / (uint32_t)P.tiles_x) * 8 + (lane >> 3);
@@ -1455,8 +1456,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
             traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
         }
-    } else if (VARIANT == 2 || VARIANT == 3) {
-        constexpr bool PF = VARIANT == 3;
+    } else if (VARIANT == 2 || VARIANT == 3 || VARIANT == 10) {
+        constexpr bool PF = VARIANT == 3 || VARIANT == 10;
         float4 pA = make_float4(0.f, 0.f, 0.f, 0.f), pB = pA;
         // One wave iteration = one traversal step.  A lane whose trace ends parks until at least
         // `regen_threshold` lanes (or every live lane) are parked; the parked lanes then shade, start
@@ -1513,7 +1514,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         }
     }
 
-    if (WIDE && !PERSIST && P.probe_cost) {   // probe launch: work of this pixel; no state is written
+    if (((WIDE && !PERSIST) || VARIANT == 3) && P.probe_cost) {   // probe launch: work of this pixel; no state is written
         // counting probe: a ray's shading + generation costs about as much as 16 child-box tests, a triangle
         // test about 4 (section profile, profiles/r01h); plain probe: rays
         if (valid) P.probe_cost[pix] = COUNT ? (16u * S.rays + cnt.boxes + 4u * cnt.tris) >> 3 : S.rays;
@@ -2440,7 +2441,7 @@ struct crt_renderer {
     int probe_min_spp = 64;        // renders with fewer samples per pixel skip the probe
     int tile_key_mode = 2;         // variant 8: see crt_tile_cost_kernel (2: measured best, profiles/r01ac)
     int n_cus = 0;
-    int variant = 3;               // see crt_renderer_set_kernel_variant
+    int variant = -1;              // see crt_renderer_set_kernel_variant; -1 = automatic
     unsigned long long diag[3] = {0, 0, 0};
     unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // COUNT-mode section profile (variant 4)
     int regen_threshold = 24;      // variants 2/3
@@ -2852,8 +2853,8 @@ int crt_renderer_init_rand(crt_renderer* R, unsigned long long seed, unsigned lo
 }
 
 int crt_renderer_set_kernel_variant(crt_renderer* R, int variant) {
-    if (!R || variant < 0 || variant > 8 || variant == 5 || variant == 6)
-        return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant (0-4, 7, 8)");
+    if (!R || variant < -1 || variant > 10 || variant == 5 || variant == 6 || variant == 9)
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant (-1 = automatic, 0-4, 7, 8, 10)");
     R->variant = variant;
     return CRT_OK;
 }
@@ -2979,6 +2980,11 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     // pixel queue) for short renders such as the 1-spp interactive frames
     int wv = R->variant;
     if (S->width == 4 && wv != 4 && wv != 7 && wv != 8) wv = probe_spp_for(R, spp) > 0 ? 8 : 7;
+    // threaded scenes (the bit-exact reference BVH, rebuilt width 2): variants 0-3 and 10 when selected explicitly;
+    // otherwise 10 (variant 3 over probe-ordered 8x8 tiles, one wave per workgroup; -17 %, profiles/r03s) when the
+    // render runs the cost probe, else 3
+    int tv = R->variant;
+    if (S->width != 4 && !(tv >= 0 && tv <= 3) && tv != 10) tv = probe_spp_for(R, spp) > 0 ? 10 : 3;
     if (R->tile_shards > 1) {
         // pixel sharding: variant 8 renders this shard's tiles; every other pixel of the framebuffer is 0, so the sum
         // of the shards' framebuffers (one collective) is the unsharded frame exactly (x + 0 = x)
@@ -3114,9 +3120,54 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         else if (occ >= 4) CRT_LAUNCH(4, 4);
         else CRT_LAUNCH(4, 1);
     }
-    else if (R->variant == 0) CRT_LAUNCH(0, 1);
-    else if (R->variant == 1) CRT_LAUNCH(1, 1);
-    else if (R->variant >= 3) {   // 4-5 on a threaded (width-2) scene: its best kernel, variant 3
+    else if (tv == 10) {
+        // variant 3's wave program (threaded BVHs, the bit-exact reference mode) scheduled like variant 8: one 8x8 tile
+        // per one-wave workgroup, most expensive first by a cost probe (variant 3's counting kernel, read-only)
+        const size_t n_pix = (size_t)R->width * R->height;
+        const int tiles_x = (R->width + 7) / 8, n_tiles = tiles_x * ((R->height + 7) / 8);
+        if (!R->d_tile_key) {
+            HIP_TRY(hipStreamSynchronize(st));
+            if (!R->d_order) {
+                HIP_TRY(hipMalloc((void**)&R->d_order, std::max(n_pix, (size_t)n_tiles * 64) * 4));
+                HIP_TRY(hipMalloc((void**)&R->d_queue, 4));
+                HIP_TRY(hipMalloc((void**)&R->d_tile_cost, n_pix * 4));
+                HIP_TRY(hipMalloc((void**)&R->d_order_hist, ORDER_KEYS * 4));
+                HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
+            }
+            HIP_TRY(hipMalloc((void**)&R->d_tile_key, (size_t)n_tiles * 4));
+        }
+        P.tiles_x = tiles_x;
+        P.order = nullptr;
+        if (probe_spp_for(R, spp) > 0) {
+            RenderParams Q = P;
+            Q.spp = probe_spp_for(R, spp);
+            Q.accumulate = 0;
+            Q.probe_cost = R->d_tile_cost;
+            hipLaunchKernelGGL((crt_render_kernel<true, 3, 5>), grid, block, 0, st, Q);
+            hipLaunchKernelGGL(crt_tile_cost_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_tile_cost,
+                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode);
+            if (R->tile_key_mode == 2) {
+                hipLaunchKernelGGL(crt_tile_neighbour_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st,
+                                   R->d_tile_key, tiles_x, n_tiles, R->d_tile_cost);
+                HIP_TRY(hipMemcpyAsync(R->d_tile_key, R->d_tile_cost, (size_t)n_tiles * 4, hipMemcpyDeviceToDevice, st));
+            }
+            const unsigned ob = (unsigned)((n_tiles + ORDER_ITEMS - 1) / ORDER_ITEMS);
+            HIP_TRY(hipMemsetAsync(R->d_order_hist, 0, ORDER_KEYS * 4, st));
+            hipLaunchKernelGGL(crt_order_hist_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key, n_tiles, R->d_order_hist);
+            hipLaunchKernelGGL(crt_order_scan_kernel, dim3(1), dim3(ORDER_KEYS), 0, st, R->d_order_hist);
+            hipLaunchKernelGGL(crt_order_scatter_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key, n_tiles,
+                               R->d_order_hist, R->d_order, 0u);
+            P.order = R->d_order;
+        }
+        const dim3 tgrid(n_tiles), tblock(64);
+        std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 10, 5>", cnt ? "true" : "false");
+        HIP_TRY(hipEventRecord(R->ev_main, st));
+        if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 10, 5>), tgrid, tblock, 0, st, P);
+        else hipLaunchKernelGGL((crt_render_kernel<false, 10, 5>), tgrid, tblock, 0, st, P);
+    }
+    else if (tv == 0) CRT_LAUNCH(0, 1);
+    else if (tv == 1) CRT_LAUNCH(1, 1);
+    else if (tv == 3) {
         if (occ >= 5) CRT_LAUNCH(3, 5);
         else if (occ >= 4) CRT_LAUNCH(3, 4);
         else CRT_LAUNCH(3, 1);

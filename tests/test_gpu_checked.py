@@ -117,3 +117,25 @@ def test_render_phase_timings(device_scenes):
     r.render(sc, 8, 20)                        # no probe: the main kernel is the whole render
     t = r.last_timings()
     assert t["probe_sort_ms"] < 0.05 and abs(t["render_ms"] - t["main_kernel_ms"]) < 0.05
+
+
+@pytest.mark.parametrize("w,h,spp", [(96, 64, 64), (100, 37, 70), (40, 24, 8)])
+def test_variant10_reference_bvh_bit_exact(device_scenes, oracle_scenes, w, h, spp):
+    """Variant 10 (variant 3's wave program on the reference's own BVHs, scheduled like variant 8: one 8x8 tile per
+    one-wave workgroup, most expensive first by a variant-3 cost probe at spp >= 64) renders the oracle's frame bit for
+    bit, ragged sizes included."""
+    _, ref = device_scenes["cornell_bunny"]
+    r = crt_amd.Renderer(w, h)
+    cam = crt_amd.camera(spp)
+    r.set_camera(cam)
+    r.set_kernel_variant(10)
+    r.init_rand(41)
+    r.render(ref, spp, 20)
+    r.resolve(crt_amd.pixel_sample_scale(spp))
+    r.synchronize()
+    assert r.last_kernel_name() == "crt_render_kernel<false, 10, 5>"
+    assert r.last_timings()["main_kernel_ms"] > 0
+    o_sum, o_rgba, o_cnt = oracle_scenes["cornell_bunny"].render(crt_amd.camera_floats(cam), w, h, spp, 20)
+    assert np.array_equal(r.linear().view(np.uint32), o_sum.view(np.uint32))
+    assert np.array_equal(r.rgba8(), o_rgba)
+    assert r.counters()["rays"] == o_cnt["rays"]

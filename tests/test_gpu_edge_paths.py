@@ -159,7 +159,7 @@ def test_edge_scenes_exercise_the_paths(edge_scenes):
 
 
 @pytest.mark.parametrize("case", list(EDGE))
-@pytest.mark.parametrize("variant", [0, 3])
+@pytest.mark.parametrize("variant", [0, 3, 10])
 def test_edge_scene_reference_bvh_bit_exact(edge_scenes, case, variant):
     _, ref, _, osc, _ = edge_scenes[case]
     w, h, spp = 160, 90, 16

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 RMS_TOL = 1e-4
 
 
-VARIANTS = [0, 1, 2, 3]
+VARIANTS = [0, 1, 2, 3, 10]   # 10: variant 3 over one-wave 8x8 tiles (probe order at spp >= 64)
 
 
 def _render(dev_scene, w, h, spp, bounces, seed=41, subseq=0, cam=None, variant=2):
