@@ -262,6 +262,12 @@ int  crt_renderer_set_regen_threshold(crt_renderer* r, int lanes);
  * regeneration threshold.  A frame with few tiles per wave slot ends with its most expensive tile, whose pixels' sample
  * chains are sequential; waiting less for the wave's other lanes shortens that chain.  Results never depend on it. */
 int  crt_renderer_set_critical_tiles(crt_renderer* r, int tiles, int lanes);
+/* 4-wide variants (4, 7, 8): a new ray's first `levels` node steps -- the root's, then the one of the internal child it
+ * continues to -- run in the regeneration pass from a copy of those nodes in LDS instead of in traversal steps that
+ * load them through L1/L2 (-1 = the compiled default, 1; at most the compiled CRT_TOP_LEVELS).  The box tests, their
+ * order and the stack entries are the traversal's own, so results never depend on it (a ray whose step hits a leaf
+ * child takes that node through the regular step). */
+int  crt_renderer_set_top_levels(crt_renderer* r, int levels);
 /* Pixel sharding, the bit-exact multi-GPU mode: renders of this renderer draw only shard `shard` of
  * `shards` -- every shards-th 8x8 tile of the cost order (or of row order without the probe) -- with all samples, and
  * leave every other pixel of the linear framebuffer at 0.  Summing the shards' framebuffers (the same reduce as spp

@@ -227,6 +227,10 @@ class Renderer:
     def set_critical_tiles(self, tiles: int = -1, lanes: int = 16):
         check(_lib.hip().crt_renderer_set_critical_tiles(self.h, int(tiles), int(lanes)), "set_critical_tiles")
 
+    def set_top_levels(self, levels: int = -1):
+        """4-wide kernels: a new ray's first node steps from the LDS copy of the tree's top nodes (-1 = default)."""
+        check(_lib.hip().crt_renderer_set_top_levels(self.h, int(levels)), "set_top_levels")
+
     def set_pixel_shard(self, shard: int = 0, shards: int = 1):
         """Render only every shards-th 8x8 tile (from shard) with all samples; other pixels stay 0 (bit-exact
         multi-GPU mode, crt_renderer_set_pixel_shard)."""

@@ -107,6 +107,7 @@ HIP_SYMBOLS = [
     "crt_renderer_attach_linear", "crt_renderer_set_kernel_variant", "crt_renderer_get_schedule_stats",
     "crt_renderer_set_regen_threshold", "crt_renderer_set_occupancy_target",
     "crt_build_mesh_bvh", "crt_renderer_set_schedule", "crt_renderer_set_critical_tiles", "crt_renderer_set_pixel_shard",
+    "crt_renderer_set_top_levels",
     "crt_selftest_math", "crt_selftest_rng", "crt_selftest_geometry", "crt_selftest_scan", "crt_selftest_rcp",
     "crt_selftest_uv_div", "crt_selftest_sqrt",
 ]
@@ -174,6 +175,7 @@ def hip():
             "crt_renderer_set_occupancy_target": ([P, i32], i32),
             "crt_renderer_set_schedule": ([P, i32, i32, i32], i32),
             "crt_renderer_set_critical_tiles": ([P, i32, i32], i32),
+            "crt_renderer_set_top_levels": ([P, i32], i32),
             "crt_build_mesh_bvh": ([i32, P, C.c_uint32, P, P, C.c_uint32, P, P, P, P], i32),
             "crt_selftest_math": ([P, P, i32, P, P], i32),
             "crt_selftest_geometry": ([i32, P, i32, P, i32, i32, P, P], i32),

@@ -16,6 +16,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "crt_hip.h"
@@ -77,6 +78,7 @@ struct RenderParams {
     uint32_t* __restrict__ probe_cost;    // probe launch (variant 4): rays per pixel; nothing else is written
     int crit_tiles, crit_threshold;       // variant 8: the first crit_tiles tiles of the cost order regenerate at
                                           // crit_threshold parked lanes instead of regen_threshold
+    int top_levels;                       // 4-wide variants: a new ray's first node steps taken from LDS (<= CRT_TOP_LEVELS)
 };
 
 #ifdef CRT_PROFILE_PAIRS
@@ -280,8 +282,21 @@ struct WaveLds {
 #endif
     int prefix[64];                  // first pair index of each owner's leaf
     unsigned char owner_at[64];      // owner lane of the pair that starts at each slot of a round
+};
+// The 4-wide kernels' per-wave LDS (traverse_step4): WaveLds without the owners' pair prefixes, which the fast build
+// keeps in the ray records (ray1.w), so the 256 B go to the top nodes (CRT_TOP_LEVELS) within occupancy 6.
+struct WaveLdsWide {
+    float4 ray0[64];
+    float4 ray1[64];
+#ifdef CRT_LEAF_DUMMY
+    unsigned long long key[128];
+#else
+    unsigned long long key[64];
+#endif
+    unsigned char owner_at[64];
 #ifdef CRT_CHECKED
-    int span_n[64];                  // checked build: each owner's pair count (its first pair is prefix[owner])
+    int prefix[64];                  // checked build: each owner's first pair index and pair count
+    int span_n[64];
 #endif
 };
 
@@ -601,6 +616,9 @@ __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, 
 // following slots are leaves whose primitives are consecutive from leaf_first in slot order; empty slots
 // have a zero-thickness box far away (never hit).
 constexpr int STACK_LDS = 16;   // per-lane traversal-stack entries kept in LDS; deeper entries go to P.ovf
+#ifndef CRT_STACK6
+#define CRT_STACK6 12           // entries at occupancy 6 (6 one-wave workgroups per SIMD within 160 KiB: <= 6144 B each)
+#endif
 
 struct Wide4 {
     float tmin[4];
@@ -940,7 +958,7 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
 
 template <bool COUNT>
 __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
-                                               float& closest, int& hit, TraceCounts& cnt, WaveLds& L,
+                                               float& closest, int& hit, TraceCounts& cnt, WaveLdsWide& L,
                                                uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix) {
     if (COUNT) cnt.step_slots++;
     const uint64_t c0 = COUNT ? shader_clock() : 0;
@@ -1032,6 +1050,76 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         }
     }
     if (COUNT) cnt.cyc_round += shader_clock() - c1;
+}
+
+// The tree's top nodes held in LDS (CRT_TOP_LEVELS): the root and, at level 2, its internal children, copied once
+// per workgroup with their rows unswizzled (row k at 16-B slot k).  Every ray starts at the root, and its first node
+// steps are the same for every ray up to the direction signs, so a new ray takes them in the regeneration pass from
+// LDS instead of in traversal steps that wait for L1/L2: the same box tests with the same operands (closest = inf,
+// no leaf was tested yet), the same near-first order and stack entries, hence the same traversal bit for bit.
+#ifndef CRT_TOP_LEVELS
+#define CRT_TOP_LEVELS 1
+#endif
+constexpr int TOP_NODES = CRT_TOP_LEVELS >= 2 ? 5 : CRT_TOP_LEVELS >= 1 ? 1 : 0;
+
+// One node step of node_step4 on an LDS record, for a lane whose ray has tested no leaf yet (closest = inf).  Returns
+// false, changing nothing, when a leaf child is hit: the lane then takes this node through the regular step, whose
+// leaf rounds test it.
+template <bool COUNT>
+__device__ __forceinline__ bool top_step4(const RenderParams& P, const float4* rec, V3 o, V3 inv, uint32_t rows,
+                                          int& node, int& sp, TraceCounts& cnt, uint32_t* __restrict__ stk,
+                                          size_t pix, size_t n_pix) {
+    const Wide4 w = wide_boxes(rec, 0u, rows, o, inv, __builtin_inff());
+    const float4 mf = rec[6];
+    const int first_child = __float_as_int(mf.x);
+    const int meta = __float_as_int(mf.y);
+    const int n_int = meta & 0xff;
+    uint32_t hm = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) hm |= w.hit[s] ? (1u << s) : 0u;
+    if (hm & (0xfu << n_int)) return false;
+    if (COUNT) cnt.boxes += (uint32_t)(meta >> 8);
+    uint32_t k[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) k[s] = (s < n_int && w.hit[s]) ? ((__float_as_uint(w.tmin[s]) & ~3u) | s) : ~0u;
+    cas(k[0], k[1]); cas(k[2], k[3]); cas(k[0], k[2]); cas(k[1], k[3]); cas(k[1], k[2]);
+    auto store = [&](int at, uint32_t v) -> bool {
+        if (at < P.stack_lds) stk[at * 64 + lane_fresh()] = v;
+        else if (at < P.stack_cap) *ovf_slot(P, at, pix, n_pix) = v;
+        else { atomicOr(P.err, 2u); return false; }
+        return true;
+    };
+    if (k[0] != ~0u) {
+        node = first_child + (int)(k[0] & 3);
+        const uint32_t n_rest = (uint32_t)__popc(hm & ((1u << n_int) - 1u)) - 1u;
+        if (n_rest && store(sp, ((uint32_t)first_child << 8) | (n_rest << 6) | ((k[1] & 3) << 4) |
+                                    ((k[2] & 3) << 2) | (k[3] & 3)))
+            ++sp;
+    } else if (sp > 0) {
+        const int at = sp - 1;
+        const uint32_t top = at < P.stack_lds ? stk[at * 64 + lane_fresh()]
+                                              : (at < P.stack_cap ? *ovf_slot(P, at, pix, n_pix) : 0u);
+        const uint32_t rest = (top >> 6) & 3;
+        node = (int)(top >> 8) + (int)((top >> 4) & 3);
+        if (rest <= 1) sp = at;
+        else store(at, (top & ~0xffu) | ((rest - 1) << 6) | ((top & 0xfu) << 2));
+    } else {
+        node = -1;
+    }
+    return true;
+}
+
+// A new ray's first node steps from the LDS top nodes: the root, then (TOPN = 5) the internal child it continues to.
+template <bool COUNT, int TOPN>
+__device__ __forceinline__ void top_steps(const RenderParams& P, const float4* top, V3 o, V3 inv, uint32_t rows,
+                                          int& node, int& sp, TraceCounts& cnt, uint32_t* __restrict__ stk, size_t pix,
+                                          size_t n_pix) {
+    if (P.top_levels <= 0) return;   // uniform
+    if (!top_step4<COUNT>(P, top, o, inv, rows, node, sp, cnt, stk, pix, n_pix) || TOPN < 5 || P.top_levels < 2 ||
+        node < 0)
+        return;
+    const int m = node - __float_as_int(top[6].x);   // node is an internal child of the root: slot m < 4
+    if ((unsigned)m < 4u) top_step4<COUNT>(P, top + 8 * (1 + m), o, inv, rows, node, sp, cnt, stk, pix, n_pix);
 }
 
 // Per-lane path state of one pixel (rayColor's locals, CUDAKernels.h:102-145, plus the sample loop).
@@ -1211,22 +1299,38 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     const unsigned long long prof_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
     constexpr int WGW = KernelShape<VARIANT>::waves;
-    __shared__ WaveLds lds[VARIANT >= 1 ? WGW : 1];
     // variant 4: 16 LDS stack entries per lane at 5 waves/SIMD; 12 at 6+ so 6 workgroups fit the 160 KiB
     constexpr bool PERSIST = VARIANT == 7;
     constexpr bool TILED = VARIANT == 8;    // variant 4 with one wave per workgroup and a tile order
     constexpr bool TILES = TILED || VARIANT == 10;   // one 8x8 tile per one-wave workgroup (variant 10: variant 3's program)
     constexpr bool WIDE = VARIANT == 4 || PERSIST || TILED;
-    constexpr int SD = WIDE ? (MINW >= 7 ? 11 : MINW >= 6 ? 12 : STACK_LDS) : 1;
+    using Lds = std::conditional_t<WIDE, WaveLdsWide, WaveLds>;
+    __shared__ Lds lds[VARIANT >= 1 ? WGW : 1];
+    constexpr int SD = WIDE ? (MINW >= 7 ? 11 : MINW >= 6 ? CRT_STACK6 : STACK_LDS) : 1;
     __shared__ uint32_t stack_lds[WIDE ? WGW * SD * 64 : 1];
     // the two per-ray spheres in 16-B rows, so every read is one ds_read_b128 at a fixed offset: per sphere
     // (center.xyz, radius^2) (box lo.xyz, box hi.x) (box hi.yz, rank, 0) (unused)
     __shared__ __attribute__((aligned(16))) float sph_lds[32];
+    constexpr int TOPN = WIDE ? TOP_NODES : 0;
+    __shared__ float4 top_lds[TOPN > 0 ? 8 * TOPN : 1];   // CRT_TOP_LEVELS: root, then its internal children
+#ifdef CRT_LDS_PAD
+    __shared__ float4 pad_lds[CRT_LDS_PAD / 16];          // experiment: LDS footprint alone
+    __asm__ volatile("" : : "v"(&pad_lds[threadIdx.x & 1]));
+#endif
     if (WIDE) {
         if (threadIdx.x < 32) {
             const int k = threadIdx.x & 15;
             const int src = k < 4 ? k : k < 9 ? k + 1 : k == 9 ? 10 : k == 10 ? 4 : -1;
             sph_lds[threadIdx.x] = src < 0 ? 0.f : P.sph2[threadIdx.x >> 4][src];
+        }
+        if (TOPN > 0 && threadIdx.x < 8u * TOPN) {
+            const uint32_t m = threadIdx.x >> 3, k = threadIdx.x & 7;
+            int n = 0;
+            if (m > 0) {   // internal child m - 1 of the root (BFS emission: consecutive from first_child)
+                const float4 rm = node_row(P.nodes, node_base(0), 6);
+                n = (int)(m - 1) < (__float_as_int(rm.y) & 0xff) ? __float_as_int(rm.x) + (int)(m - 1) : -1;
+            }
+            if (n >= 0 && n < P.n_nodes) top_lds[threadIdx.x] = node_row(P.nodes, node_base(n), k);
         }
         __syncthreads();
     }
@@ -1273,7 +1377,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t wave_rays = 0;    // variant 8: rays of the wave (uniform); the other variants count per lane
 
-    if (VARIANT == 0) {
+    if constexpr (VARIANT == 0) {
         for (;;) {
             if (!next_ray(S, C, x, y, P.max_bounces)) break;
             ++S.rays;
@@ -1282,12 +1386,12 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                                          S.d, t, cnt);
             shade(S, P, hit, t);
         }
-    } else if (PERSIST) {
+    } else if constexpr (PERSIST) {
         // Variant 4's scheduling, but a lane whose pixel has no samples left stores it and takes the next
         // pixel slot from the global queue (8x8 tiles in `order`, most expensive first), so lanes never wait
         // for their wave's slowest pixel and waves never wait for their workgroup or the launch's last tiles.
         // Each pixel is still traced by ONE lane, samples in order, from its own RNG stream: same results.
-        WaveLds& L = lds[wave];
+        auto& L = lds[wave];
         uint32_t* stk = stack_lds + wave * SD * 64;
         const float INF = __builtin_inff();
         const size_t n_pix = (size_t)P.width * P.height;
@@ -1376,15 +1480,16 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     if (COUNT) cnt.spheres += P.n_ray_spheres;
                     L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                     if (COUNT) cnt.trace_calls++;
+                    if (TOPN > 0) top_steps<COUNT, TOPN>(P, top_lds, S.o, inv, rows, node, sp, cnt, stk, (size_t)ppix, n_pix);
                 }
                 if (!wave_ballot(live)) break;      // the queue is empty and every lane is done
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
             traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)ppix, n_pix);
         }
-    } else if (WIDE) {
+    } else if constexpr (WIDE) {
         // Same scheduling as variant 3 over a 4-wide BVH: node < 0 = no node left (lane parked).
-        WaveLds& L = lds[wave];
+        auto& L = lds[wave];
         uint32_t* stk = stack_lds + wave * SD * 64;
         const float INF = __builtin_inff();
         const size_t n_pix = (size_t)P.width * P.height;
@@ -1446,6 +1551,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         if (COUNT) cnt.spheres += P.n_ray_spheres;
                         L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                         if (COUNT) cnt.trace_calls++;
+                        if (TOPN > 0) top_steps<COUNT, TOPN>(P, top_lds, S.o, inv, rows, node, sp, cnt, stk, (size_t)pix, n_pix);
                     }
                 }
                 live_mask = wave_ballot(has_result);
@@ -1456,13 +1562,13 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
             traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
         }
-    } else if (VARIANT == 2 || VARIANT == 3 || VARIANT == 10) {
+    } else if constexpr (VARIANT == 2 || VARIANT == 3 || VARIANT == 10) {
         constexpr bool PF = VARIANT == 3 || VARIANT == 10;
         float4 pA = make_float4(0.f, 0.f, 0.f, 0.f), pB = pA;
         // One wave iteration = one traversal step.  A lane whose trace ends parks until at least
         // `regen_threshold` lanes (or every live lane) are parked; the parked lanes then shade, start
         // their next ray and rejoin traversal while the others keep stepping.
-        WaveLds& L = lds[wave];
+        auto& L = lds[wave];
         const float INF = __builtin_inff();
         bool live = true, has_result = false;
         int node = P.n_nodes, hit = -1, nbase = 0;
@@ -2449,6 +2555,7 @@ struct crt_renderer {
     int crit_tiles = -1;           // variant 8: leading tiles of the cost order regenerating at crit_threshold; -1 = 4 per CU
     int tile_shard = 0, tile_shards = 1;   // pixel sharding (crt_renderer_set_pixel_shard)
     int crit_threshold = 16;       // (measured: profiles/r02h, r02i)
+    int top_levels = -1;           // 4-wide variants: new rays' first node steps from LDS; -1 = CRT_TOP_LEVELS
     int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 6 for 4-wide scenes, 5 otherwise
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
     size_t ovf_entries = 0;
@@ -2876,6 +2983,13 @@ int crt_renderer_set_pixel_shard(crt_renderer* R, int shard, int shards) {
     return CRT_OK;
 }
 
+int crt_renderer_set_top_levels(crt_renderer* R, int levels) {
+    if (!R || levels < -1 || levels > CRT_TOP_LEVELS)
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "top levels -1 (default) .. " + std::to_string(CRT_TOP_LEVELS));
+    R->top_levels = levels;
+    return CRT_OK;
+}
+
 int crt_renderer_set_critical_tiles(crt_renderer* R, int tiles, int lanes) {
     if (!R || tiles < -1 || lanes < 1 || lanes > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "critical tiles >= -1, lanes 1..64");
     R->crit_tiles = tiles;
@@ -2938,6 +3052,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.rcp_w = R->rcp_w; P.rcp_h = R->rcp_h; P.fast_uv = R->fast_uv;
     P.ovf = nullptr;
     P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0; P.crit_tiles = 0; P.crit_threshold = 64;
+    P.top_levels = R->top_levels < 0 ? CRT_TOP_LEVELS : R->top_levels;
     P.stack_cap = S->stack_cap;
     P.sphere_first = S->sphere_first;
     P.n_ray_spheres = S->n_ray_spheres;
@@ -2946,7 +3061,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.tree_spheres = S->tree_spheres;
     std::memcpy(P.sph2, S->sph2, sizeof P.sph2);
     const int occ = R->min_waves ? R->min_waves : (S->width == 4 ? 6 : 5);
-    P.stack_lds = std::min(R->stack_lds, occ >= 7 ? 11 : occ >= 6 ? 12 : STACK_LDS);
+    P.stack_lds = std::min(R->stack_lds, occ >= 7 ? 11 : occ >= 6 ? CRT_STACK6 : STACK_LDS);
     // a stack_cap override below the LDS entries must still report the entries it drops (crt_scene_options.stack_cap)
     if (S->width == 4 && S->stack_cap > 0) P.stack_lds = std::min(P.stack_lds, S->stack_cap);
     if (S->width == 4 && S->stack_cap > P.stack_lds) {

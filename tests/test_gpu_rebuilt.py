@@ -231,3 +231,33 @@ def _schedule_case(rebuilt, variant, probe_spp, crit=None, **flags):
     b.synchronize()
     assert np.array_equal(a.linear().view(np.uint32), b.linear().view(np.uint32))
     assert np.array_equal(a.rng_state(), b.rng_state())
+
+
+@pytest.mark.parametrize("variant,spp,count", [(8, 64, False), (4, 8, False), (7, 8, False), (8, 4, True), (7, 4, True)])
+def test_top_levels_are_bit_identical(rebuilt, variant, spp, count):
+    """A new ray's first node step from the LDS copy of the root (crt_renderer_set_top_levels, the default) against
+    the regular traversal step over the same node: the same frame, RNG state and work counters (box tests included)."""
+    dev = rebuilt["cornell_bunny", "w4"]
+    w, h = 104, 45
+    out = []
+    for levels in (0, -1):
+        r = crt_amd.Renderer(w, h)
+        r.set_kernel_variant(variant)
+        r.set_top_levels(levels)
+        r.set_camera(crt_amd.camera(spp))
+        r.init_rand(41)
+        r.render(dev, spp, 20, count_work=count)
+        r.synchronize()
+        out.append((r.linear().view(np.uint32), r.rng_state(), r.counters()))
+    (a_lin, a_rng, a_c), (b_lin, b_rng, b_c) = out
+    assert np.array_equal(a_lin, b_lin) and np.array_equal(a_rng, b_rng)
+    keys = ("rays", "box_tests", "tri_tests", "sphere_tests", "paths") if count else ("rays",)
+    for k in keys:
+        assert a_c[k] == b_c[k], k
+
+
+def test_top_levels_rejects_bad_arguments():
+    r = crt_amd.Renderer(16, 16)
+    for levels in (-2, 9):
+        with pytest.raises(crt_amd.CrtError):
+            r.set_top_levels(levels)
