@@ -1214,19 +1214,34 @@ __device__ __forceinline__ bool cannot_refract_exact(float cos_theta, float ri) 
 
 // Phase 3: material scatter / emit / sky (CUDAKernels.h:123-142, Material.cuh:66-146).  The hit's normal and
 // material come from its shading record (crt_device.h): one pair of independent loads per hit.
+// shade_rec: the same with the hit's shading record rows 0-1 already loaded (r0, m); a sphere's row 2 (1 / radius) is
+// inv_r when `staged`, else loaded here.
+__device__ __forceinline__ void shade_rec(PathState& S, const RenderParams& P, int hit_rank, float t, float4 r0,
+                                          float4 m, bool staged, float inv_r);
 __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int hit_rank, float t) {
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), m = r0;
+    if (hit_rank >= 0) {
+        const float4* R = P.shade + 3u * (uint32_t)hit_rank;   // 32-bit index (ranks < 2^30): no 64-bit multiply
+        r0 = R[0];
+        m = R[1];
+    }
+    shade_rec(S, P, hit_rank, t, r0, m, false, 0.f);
+}
+__device__ __forceinline__ void shade_rec(PathState& S, const RenderParams& P, int hit_rank, float t, float4 r0,
+                                          float4 m, bool staged, float inv_r) {
     if (hit_rank < 0) {                                  // :137-142
         S.pixel = S.pixel + S.thr * sky(S.d);
         ++S.paths;
         S.need_new = true;
         return;
     }
-    const float4* R = P.shade + 3u * (uint32_t)hit_rank;   // 32-bit index (ranks < 2^30): no 64-bit multiply
-    const float4 r0 = R[0], m = R[1];
     const uint32_t kind = __float_as_uint(r0.w);
     const V3 hp = S.o + t * S.d;                         // Ray::pointAtDistance
     V3 outward = v3(r0.x, r0.y, r0.z);                   // triangle: unit(cross(e1, e2)), Mesh.cuh:303-304
-    if (kind & SHADE_SPHERE) outward = R[2].x * (hp - outward);   // Sphere.cuh:44: (1 / radius) * (p - center)
+    if (kind & SHADE_SPHERE) {                           // Sphere.cuh:44: (1 / radius) * (p - center)
+        const float ir = staged ? inv_r : P.shade[3u * (uint32_t)hit_rank + 2u].x;
+        outward = ir * (hp - outward);
+    }
     const bool front = dot(S.d, outward) < 0;            // HitInfo::setFaceNormal
     const V3 n = front ? outward : -outward;
     const uint32_t code = kind & 15u;
@@ -1312,6 +1327,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     // (center.xyz, radius^2) (box lo.xyz, box hi.x) (box hi.yz, rank, 0) (unused)
     __shared__ __attribute__((aligned(16))) float sph_lds[32];
     constexpr int TOPN = WIDE ? TOP_NODES : 0;
+    // the two per-ray spheres' shading records (3 rows each), so a pass whose sphere test overrides the trace's hit
+    // reads the record from LDS (the trace's own hit record is loaded at the pass start)
+    __shared__ float4 shd_lds[WIDE ? 6 : 1];
     __shared__ float4 top_lds[TOPN > 0 ? 8 * TOPN : 1];   // CRT_TOP_LEVELS: root, then its internal children
 #ifdef CRT_LDS_PAD
     __shared__ float4 pad_lds[CRT_LDS_PAD / 16];          // experiment: LDS footprint alone
@@ -1322,6 +1340,10 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             const int k = threadIdx.x & 15;
             const int src = k < 4 ? k : k < 9 ? k + 1 : k == 9 ? 10 : k == 10 ? 4 : -1;
             sph_lds[threadIdx.x] = src < 0 ? 0.f : P.sph2[threadIdx.x >> 4][src];
+        }
+        if (threadIdx.x >= 32 && threadIdx.x < 38 && P.n_ray_spheres == 2) {
+            const uint32_t q = threadIdx.x - 32, sp = q / 3;
+            shd_lds[q] = P.shade[3u * (uint32_t)__float_as_int(P.sph2[sp][4]) + q % 3];
         }
         if (TOPN > 0 && threadIdx.x < 8u * TOPN) {
             const uint32_t m = threadIdx.x >> 3, k = threadIdx.x & 7;
@@ -1523,10 +1545,35 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     // the lanes with a ray): a uniform test instead of a divergent branch on has_result (-0.38 %,
                     // profiles/r02av)
                     if (!first_pass) {
+                        // the trace's hit record, loaded before the per-ray sphere test so its latency hides behind it
+                        // (-0.6 %, profiles/r03aa)
+                        const int h0 = hit;
+                        float4 e0 = make_float4(0.f, 0.f, 0.f, 0.f), e1 = e0;
+                        if (h0 >= 0) {
+                            const float4* Rh = P.shade + 3u * (uint32_t)h0;
+                            e0 = Rh[0];
+                            e1 = Rh[1];
+                        }
+                        __asm__ volatile("" : : : "memory");   // keep the loads ahead of the sphere test
                         ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o,
                                           S.d, sphere_inv(S.d, inv), closest, hit, sph_lds);
                         if (COUNT) cnt.cyc_sph += shader_clock() - s0;
-                        shade(S, P, hit, closest);
+                        bool staged = false;
+                        float inv_r = 0.f;
+                        if (hit != h0 && hit >= 0) {   // a per-ray sphere won: its record from LDS (two spheres) or HBM
+                            if (P.n_ray_spheres == 2) {
+                                const int k = hit == __float_as_int(sph_lds[26]) ? 3 : 0;
+                                e0 = shd_lds[k];
+                                e1 = shd_lds[k + 1];
+                                inv_r = shd_lds[k + 2].x;
+                                staged = true;
+                            } else {
+                                const float4* Rh = P.shade + 3u * (uint32_t)hit;
+                                e0 = Rh[0];
+                                e1 = Rh[1];
+                            }
+                        }
+                        shade_rec(S, P, hit, closest, e0, e1, staged, inv_r);
                     }
                     const uint64_t s1 = COUNT ? shader_clock() : 0;
                     const bool live = next_ray(S, C, x, y, P.max_bounces);
