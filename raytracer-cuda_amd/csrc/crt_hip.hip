@@ -1295,6 +1295,42 @@ __device__ __forceinline__ void shade_rec(PathState& S, const RenderParams& P, i
     }
 }
 
+// A parked lane's end of trace in the regeneration pass (4-wide variants): the per-ray spheres (Sphere::hit behind the
+// reference's sphere box, ray_spheres) and then shade.  The trace's own hit record is loaded before the sphere test,
+// behind a compiler barrier, so its latency hides behind that test (-0.6 %, profiles/r03aa); when a per-ray sphere
+// wins, its record comes from the LDS copy of the two per-ray spheres' records (or from HBM for other sphere counts).
+template <bool COUNT>
+__device__ __forceinline__ void finish_ray(PathState& S, const RenderParams& P, V3 inv, float closest, int hit,
+                                           const float* sph_lds, const float4* shd_lds, TraceCounts& cnt, uint64_t s0) {
+    const int h0 = hit;
+    float4 e0 = make_float4(0.f, 0.f, 0.f, 0.f), e1 = e0;
+    if (h0 >= 0) {
+        const float4* Rh = P.shade + 3u * (uint32_t)h0;
+        e0 = Rh[0];
+        e1 = Rh[1];
+    }
+    __asm__ volatile("" : : : "memory");   // keep the loads ahead of the sphere test
+    ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
+                      sphere_inv(S.d, inv), closest, hit, sph_lds);
+    if (COUNT) cnt.cyc_sph += shader_clock() - s0;
+    bool staged = false;
+    float inv_r = 0.f;
+    if (hit != h0 && hit >= 0) {   // a per-ray sphere won: its record from LDS (two spheres) or HBM
+        if (P.n_ray_spheres == 2) {
+            const int k = hit == __float_as_int(sph_lds[26]) ? 3 : 0;
+            e0 = shd_lds[k];
+            e1 = shd_lds[k + 1];
+            inv_r = shd_lds[k + 2].x;
+            staged = true;
+        } else {
+            const float4* Rh = P.shade + 3u * (uint32_t)hit;
+            e0 = Rh[0];
+            e1 = Rh[1];
+        }
+    }
+    shade_rec(S, P, hit, closest, e0, e1, staged, inv_r);
+}
+
 // VARIANT 0: per-lane traversal (leaf loops inside the lane).  VARIANT 1: cooperative leaves.
 // VARIANT 2: cooperative leaves + traversal-step scheduling.  MINW: occupancy target (waves per SIMD)
 // handed to the register allocator through __launch_bounds__.
@@ -1435,10 +1471,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             if (n_parked >= P.regen_threshold || n_parked == n_live) {
                 if (COUNT) cnt.passes++;
                 if (parked) {
-                    if (has_result)
-                        ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
-                                          sphere_inv(S.d, inv), closest, hit, sph_lds);
-                    if (has_result) shade(S, P, hit, closest);
+                    if (has_result) finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, c0);
                     live = next_ray(S, C, px, py, P.max_bounces);
                     has_result = false;
                 }
@@ -1545,35 +1578,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     // the lanes with a ray): a uniform test instead of a divergent branch on has_result (-0.38 %,
                     // profiles/r02av)
                     if (!first_pass) {
-                        // the trace's hit record, loaded before the per-ray sphere test so its latency hides behind it
-                        // (-0.6 %, profiles/r03aa)
-                        const int h0 = hit;
-                        float4 e0 = make_float4(0.f, 0.f, 0.f, 0.f), e1 = e0;
-                        if (h0 >= 0) {
-                            const float4* Rh = P.shade + 3u * (uint32_t)h0;
-                            e0 = Rh[0];
-                            e1 = Rh[1];
-                        }
-                        __asm__ volatile("" : : : "memory");   // keep the loads ahead of the sphere test
-                        ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o,
-                                          S.d, sphere_inv(S.d, inv), closest, hit, sph_lds);
-                        if (COUNT) cnt.cyc_sph += shader_clock() - s0;
-                        bool staged = false;
-                        float inv_r = 0.f;
-                        if (hit != h0 && hit >= 0) {   // a per-ray sphere won: its record from LDS (two spheres) or HBM
-                            if (P.n_ray_spheres == 2) {
-                                const int k = hit == __float_as_int(sph_lds[26]) ? 3 : 0;
-                                e0 = shd_lds[k];
-                                e1 = shd_lds[k + 1];
-                                inv_r = shd_lds[k + 2].x;
-                                staged = true;
-                            } else {
-                                const float4* Rh = P.shade + 3u * (uint32_t)hit;
-                                e0 = Rh[0];
-                                e1 = Rh[1];
-                            }
-                        }
-                        shade_rec(S, P, hit, closest, e0, e1, staged, inv_r);
+                        finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, s0);
                     }
                     const uint64_t s1 = COUNT ? shader_clock() : 0;
                     const bool live = next_ray(S, C, x, y, P.max_bounces);
