@@ -98,7 +98,7 @@ def parse():
     ap.add_argument("--regen-threshold", type=int, default=None,
                     help="parked lanes before a regeneration pass (default: the library's, 44 for 4-wide scenes)")
     ap.add_argument("--occupancy", type=int, default=None,
-                    help="render-kernel occupancy target in waves per SIMD (default: the library's, 6 for 4-wide scenes)")
+                    help="render-kernel occupancy target in waves per SIMD (default: the library's, 7 for variant 8)")
     ap.add_argument("--probe-spp", type=int, default=None,
                     help="cost-probe samples per pixel before a variant-8 render (default: the library's automatic "
                          "choice, 4 for >= 1000 spp else 2; 0 = no probe)")

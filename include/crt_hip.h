@@ -277,9 +277,9 @@ int  crt_renderer_set_pixel_shard(crt_renderer* r, int shard, int shards);
 /* Variant 4: per-lane traversal-stack entries kept in LDS (1..16, default 16); deeper entries spill to a
  * per-pixel region in HBM.  Results do not depend on it (tests force the HBM path with 1). */
 int  crt_renderer_set_stack_lds(crt_renderer* r, int entries);
-/* Variants 2-4: register-allocation occupancy target in waves per SIMD (1 = compiler default, 4-8;
- * 0 = auto, the default: 6 for 4-wide scenes, 5 otherwise).  At 6+ waves the 4-wide kernel keeps 12
- * (7: 11) traversal-stack entries per lane in LDS. */
+/* Register-allocation occupancy target in waves per SIMD (1 = compiler default, 4-8; 0 = auto, the default: 7 for
+ * variant 8, 6 for the other 4-wide variants, 5 for threaded scenes).  The 4-wide kernels keep 12 traversal-stack
+ * entries per lane in LDS at 6 waves and 8 at 7+ (LDS is allocated in 1-KiB steps per workgroup). */
 int  crt_renderer_set_occupancy_target(crt_renderer* r, int waves_per_simd);
 /* Trace `spp` samples per pixel continuing each pixel's RNG stream; the per-pixel
  * linear sum (pixel_color, CUDAKernels.h:157-162) is kept in an fp32 W*H*3 buffer. */

@@ -619,6 +619,11 @@ constexpr int STACK_LDS = 16;   // per-lane traversal-stack entries kept in LDS;
 #ifndef CRT_STACK6
 #define CRT_STACK6 12           // entries at occupancy 6 (6 one-wave workgroups per SIMD within 160 KiB: <= 6144 B each)
 #endif
+#ifndef CRT_STACK7
+#define CRT_STACK7 8            // entries at occupancy 7: LDS is allocated in 1-KiB steps, so 28 one-wave workgroups per
+                                // CU need <= 5,120 B each (variant 8: 5,024 B; 9 entries, 5,280 B, stay at 6 per SIMD,
+                                // profiles/r03ah)
+#endif
 
 struct Wide4 {
     float tmin[4];
@@ -1357,7 +1362,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     constexpr bool WIDE = VARIANT == 4 || PERSIST || TILED;
     using Lds = std::conditional_t<WIDE, WaveLdsWide, WaveLds>;
     __shared__ Lds lds[VARIANT >= 1 ? WGW : 1];
-    constexpr int SD = WIDE ? (MINW >= 7 ? 11 : MINW >= 6 ? CRT_STACK6 : STACK_LDS) : 1;
+    constexpr int SD = WIDE ? (MINW >= 7 ? CRT_STACK7 : MINW >= 6 ? CRT_STACK6 : STACK_LDS) : 1;
     __shared__ uint32_t stack_lds[WIDE ? WGW * SD * 64 : 1];
     // the two per-ray spheres in 16-B rows, so every read is one ds_read_b128 at a fixed offset: per sphere
     // (center.xyz, radius^2) (box lo.xyz, box hi.x) (box hi.yz, rank, 0) (unused)
@@ -2608,7 +2613,8 @@ struct crt_renderer {
     int tile_shard = 0, tile_shards = 1;   // pixel sharding (crt_renderer_set_pixel_shard)
     int crit_threshold = 16;       // (measured: profiles/r02h, r02i)
     int top_levels = -1;           // 4-wide variants: new rays' first node steps from LDS; -1 = CRT_TOP_LEVELS
-    int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 6 for 4-wide scenes, 5 otherwise
+    int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 7 for variant 8, 6 for the other 4-wide
+                                   // variants, 5 for threaded scenes
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
     size_t ovf_entries = 0;
     int stack_lds = STACK_LDS;     // variant 4: per-lane stack entries kept in LDS
@@ -3112,24 +3118,6 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.n_chain = S->n_chain;
     P.tree_spheres = S->tree_spheres;
     std::memcpy(P.sph2, S->sph2, sizeof P.sph2);
-    const int occ = R->min_waves ? R->min_waves : (S->width == 4 ? 6 : 5);
-    P.stack_lds = std::min(R->stack_lds, occ >= 7 ? 11 : occ >= 6 ? CRT_STACK6 : STACK_LDS);
-    // a stack_cap override below the LDS entries must still report the entries it drops (crt_scene_options.stack_cap)
-    if (S->width == 4 && S->stack_cap > 0) P.stack_lds = std::min(P.stack_lds, S->stack_cap);
-    if (S->width == 4 && S->stack_cap > P.stack_lds) {
-        const size_t need = (size_t)(S->stack_cap - P.stack_lds);
-        if (need * R->width * R->height * 4 >= ((size_t)1 << 32))
-            return set_error(CRT_ERR_INVALID_ARGUMENT, "traversal-stack overflow region would exceed 4 GiB");
-        if (need > R->ovf_entries) {         // grow the overflow stack region (rarely needed)
-            HIP_TRY(hipStreamSynchronize(st));
-            if (R->d_ovf) (void)hipFree(R->d_ovf);
-            R->d_ovf = nullptr;
-            R->ovf_entries = 0;
-            HIP_TRY(hipMalloc((void**)&R->d_ovf, need * R->width * R->height * 4));
-            R->ovf_entries = need;
-        }
-        P.ovf = R->d_ovf;
-    }
     dim3 grid((R->width + 15) / 16, (R->height + 15) / 16), block(256);
     const bool cnt = (flags & CRT_RENDER_COUNT_WORK) != 0;
     P.regen_threshold = S->width == 4 ? R->regen_threshold_wide : R->regen_threshold;
@@ -3152,6 +3140,27 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     // render runs the cost probe, else 3
     int tv = R->variant;
     if (S->width != 4 && !(tv >= 0 && tv <= 3) && tv != 10) tv = probe_spp_for(R, spp) > 0 ? 10 : 3;
+    // occupancy target (waves per SIMD): variant 8 runs at 7 (72 VGPRs, 8 LDS stack entries so that 28 one-wave
+    // workgroups fit a CU's LDS; -2.7 %, profiles/r03ah), the other 4-wide variants at 6, threaded scenes at 5
+    const int occ = R->min_waves ? R->min_waves
+                                 : (S->width == 4 ? ((wv == 8 || R->tile_shards > 1) ? 7 : 6) : 5);
+    P.stack_lds = std::min(R->stack_lds, occ >= 7 ? CRT_STACK7 : occ >= 6 ? CRT_STACK6 : STACK_LDS);
+    // a stack_cap override below the LDS entries must still report the entries it drops (crt_scene_options.stack_cap)
+    if (S->width == 4 && S->stack_cap > 0) P.stack_lds = std::min(P.stack_lds, S->stack_cap);
+    if (S->width == 4 && S->stack_cap > P.stack_lds) {
+        const size_t need = (size_t)(S->stack_cap - P.stack_lds);
+        if (need * R->width * R->height * 4 >= ((size_t)1 << 32))
+            return set_error(CRT_ERR_INVALID_ARGUMENT, "traversal-stack overflow region would exceed 4 GiB");
+        if (need > R->ovf_entries) {         // grow the overflow stack region (rarely needed)
+            HIP_TRY(hipStreamSynchronize(st));
+            if (R->d_ovf) (void)hipFree(R->d_ovf);
+            R->d_ovf = nullptr;
+            R->ovf_entries = 0;
+            HIP_TRY(hipMalloc((void**)&R->d_ovf, need * R->width * R->height * 4));
+            R->ovf_entries = need;
+        }
+        P.ovf = R->d_ovf;
+    }
     if (R->tile_shards > 1) {
         // pixel sharding: variant 8 renders this shard's tiles; every other pixel of the framebuffer is 0, so the sum
         // of the shards' framebuffers (one collective) is the unsharded frame exactly (x + 0 = x)

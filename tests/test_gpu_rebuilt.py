@@ -186,7 +186,7 @@ def test_persistent_queue_counting_kernel(rebuilt, variant):
     for k in ("rays", "box_tests", "tri_tests", "sphere_tests", "paths"):
         assert ca[k] == cb[k], k
     assert np.array_equal(a.linear().view(np.uint32), b.linear().view(np.uint32))
-    assert b.last_kernel_name() == f"crt_render_kernel<true, {variant}, 6>"
+    assert b.last_kernel_name() == f"crt_render_kernel<true, {variant}, {7 if variant == 8 else 6}>"
 
 
 @pytest.mark.parametrize("probe_spp", [0, 4])
