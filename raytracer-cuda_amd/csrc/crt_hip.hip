@@ -2613,8 +2613,8 @@ struct crt_renderer {
     int tile_shard = 0, tile_shards = 1;   // pixel sharding (crt_renderer_set_pixel_shard)
     int crit_threshold = 16;       // (measured: profiles/r02h, r02i)
     int top_levels = -1;           // 4-wide variants: new rays' first node steps from LDS; -1 = CRT_TOP_LEVELS
-    int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 7 for variant 8, 6 for the other 4-wide
-                                   // variants, 5 for threaded scenes
+    int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 7 for variant 8 over >= 4 tiles per wave
+                                   // slot, 6 for the other 4-wide launches, 5 for threaded scenes
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
     size_t ovf_entries = 0;
     int stack_lds = STACK_LDS;     // variant 4: per-lane stack entries kept in LDS
@@ -3141,9 +3141,16 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     int tv = R->variant;
     if (S->width != 4 && !(tv >= 0 && tv <= 3) && tv != 10) tv = probe_spp_for(R, spp) > 0 ? 10 : 3;
     // occupancy target (waves per SIMD): variant 8 runs at 7 (72 VGPRs, 8 LDS stack entries so that 28 one-wave
-    // workgroups fit a CU's LDS; -2.7 %, profiles/r03ah), the other 4-wide variants at 6, threaded scenes at 5
-    const int occ = R->min_waves ? R->min_waves
-                                 : (S->width == 4 ? ((wv == 8 || R->tile_shards > 1) ? 7 : 6) : 5);
+    // workgroups fit a CU's LDS; -2.4 % on config C, profiles/r03aj) when its frame has at least 4 tiles per wave slot,
+    // else at 6: a frame with few tiles per slot ends with its most expensive tile's sequential sample chain, which a
+    // seventh wave per SIMD slows down (config B, 2 tiles per slot: +3.3 % at 7, profiles/r03ak).  The other 4-wide
+    // variants run at 6, threaded scenes at 5.
+    int occ = R->min_waves ? R->min_waves : (S->width == 4 ? 6 : 5);
+    if (!R->min_waves && S->width == 4 && (wv == 8 || R->tile_shards > 1)) {
+        if (!R->n_cus) HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
+        const size_t tiles = (size_t)((R->width + 7) / 8) * ((R->height + 7) / 8) / (size_t)std::max(1, R->tile_shards);
+        if (tiles >= (size_t)4 * R->n_cus * 4 * 7) occ = 7;
+    }
     P.stack_lds = std::min(R->stack_lds, occ >= 7 ? CRT_STACK7 : occ >= 6 ? CRT_STACK6 : STACK_LDS);
     // a stack_cap override below the LDS entries must still report the entries it drops (crt_scene_options.stack_cap)
     if (S->width == 4 && S->stack_cap > 0) P.stack_lds = std::min(P.stack_lds, S->stack_cap);

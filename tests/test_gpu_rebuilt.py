@@ -186,7 +186,7 @@ def test_persistent_queue_counting_kernel(rebuilt, variant):
     for k in ("rays", "box_tests", "tri_tests", "sphere_tests", "paths"):
         assert ca[k] == cb[k], k
     assert np.array_equal(a.linear().view(np.uint32), b.linear().view(np.uint32))
-    assert b.last_kernel_name() == f"crt_render_kernel<true, {variant}, {7 if variant == 8 else 6}>"
+    assert b.last_kernel_name() == f"crt_render_kernel<true, {variant}, 6>"
 
 
 @pytest.mark.parametrize("probe_spp", [0, 4])
@@ -261,3 +261,25 @@ def test_top_levels_rejects_bad_arguments():
     for levels in (-2, 9):
         with pytest.raises(crt_amd.CrtError):
             r.set_top_levels(levels)
+
+
+def test_occupancy_seven_is_bit_identical_and_automatic(rebuilt):
+    """Variant 8 at 7 waves/SIMD (8 LDS stack entries, deeper entries in HBM) renders the occupancy-6 frame bit for bit;
+    the automatic choice takes 7 for a headline-sized frame (>= 4 tiles per wave slot) and 6 for a small one."""
+    dev = rebuilt["cornell_bunny", "w4"]
+    w, h, spp = 2560, 1440, 64
+    out = []
+    for occ in (6, 0):
+        r = crt_amd.Renderer(w, h)
+        if occ:
+            r.set_occupancy_target(occ)
+        r.set_camera(crt_amd.camera(spp))
+        r.init_rand(41)
+        r.render(dev, spp, 20)
+        r.synchronize()
+        out.append((r.last_kernel_name(), r.linear().view(np.uint32), r.rng_state(), r.counters()["rays"]))
+    (k6, lin6, rng6, rays6), (k7, lin7, rng7, rays7) = out
+    assert k6 == "crt_render_kernel<false, 8, 6>" and k7 == "crt_render_kernel<false, 8, 7>"
+    assert np.array_equal(lin6, lin7) and np.array_equal(rng6, rng7) and rays6 == rays7
+    small = _frame(dev, 104, 45, 64, 20, crt_amd.camera(64), variant=-1)
+    assert small.last_kernel_name() == "crt_render_kernel<false, 8, 6>"
