@@ -2614,7 +2614,7 @@ struct crt_renderer {
     int crit_threshold = 16;       // (measured: profiles/r02h, r02i)
     int top_levels = -1;           // 4-wide variants: new rays' first node steps from LDS; -1 = CRT_TOP_LEVELS
     int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 7 for variant 8 over >= 4 tiles per wave
-                                   // slot, 6 for the other 4-wide launches, 5 for threaded scenes
+                                   // slot, 6 for the other 4-wide launches and variant 10, 5 for variants 0-3
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
     size_t ovf_entries = 0;
     int stack_lds = STACK_LDS;     // variant 4: per-lane stack entries kept in LDS
@@ -3145,7 +3145,8 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     // else at 6: a frame with few tiles per slot ends with its most expensive tile's sequential sample chain, which a
     // seventh wave per SIMD slows down (config B, 2 tiles per slot: +3.3 % at 7, profiles/r03ak).  The other 4-wide
     // variants run at 6, threaded scenes at 5.
-    int occ = R->min_waves ? R->min_waves : (S->width == 4 ? 6 : 5);
+    // Variant 10 (threaded, bit-exact) runs at 6 (80 VGPRs; -8.0 % against 5, profiles/r03am).
+    int occ = R->min_waves ? R->min_waves : (S->width == 4 ? 6 : tv == 10 ? 6 : 5);
     if (!R->min_waves && S->width == 4 && (wv == 8 || R->tile_shards > 1)) {
         if (!R->n_cus) HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
         const size_t tiles = (size_t)((R->width + 7) / 8) * ((R->height + 7) / 8) / (size_t)std::max(1, R->tile_shards);
@@ -3343,10 +3344,19 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             P.order = R->d_order;
         }
         const dim3 tgrid(n_tiles), tblock(64);
-        std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 10, 5>", cnt ? "true" : "false");
+        const int w10 = occ >= 7 ? 7 : occ >= 6 ? 6 : 5;
+        std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 10, %d>", cnt ? "true" : "false", w10);
         HIP_TRY(hipEventRecord(R->ev_main, st));
-        if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 10, 5>), tgrid, tblock, 0, st, P);
-        else hipLaunchKernelGGL((crt_render_kernel<false, 10, 5>), tgrid, tblock, 0, st, P);
+        if (w10 == 7) {
+            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 10, 7>), tgrid, tblock, 0, st, P);
+            else hipLaunchKernelGGL((crt_render_kernel<false, 10, 7>), tgrid, tblock, 0, st, P);
+        } else if (w10 == 6) {
+            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 10, 6>), tgrid, tblock, 0, st, P);
+            else hipLaunchKernelGGL((crt_render_kernel<false, 10, 6>), tgrid, tblock, 0, st, P);
+        } else {
+            if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 10, 5>), tgrid, tblock, 0, st, P);
+            else hipLaunchKernelGGL((crt_render_kernel<false, 10, 5>), tgrid, tblock, 0, st, P);
+        }
     }
     else if (tv == 0) CRT_LAUNCH(0, 1);
     else if (tv == 1) CRT_LAUNCH(1, 1);

@@ -133,9 +133,28 @@ def test_variant10_reference_bvh_bit_exact(device_scenes, oracle_scenes, w, h, s
     r.render(ref, spp, 20)
     r.resolve(crt_amd.pixel_sample_scale(spp))
     r.synchronize()
-    assert r.last_kernel_name() == "crt_render_kernel<false, 10, 5>"
+    assert r.last_kernel_name() == "crt_render_kernel<false, 10, 6>"
     assert r.last_timings()["main_kernel_ms"] > 0
     o_sum, o_rgba, o_cnt = oracle_scenes["cornell_bunny"].render(crt_amd.camera_floats(cam), w, h, spp, 20)
     assert np.array_equal(r.linear().view(np.uint32), o_sum.view(np.uint32))
     assert np.array_equal(r.rgba8(), o_rgba)
+    assert r.counters()["rays"] == o_cnt["rays"]
+
+
+@pytest.mark.parametrize("occ", [5, 7])
+def test_variant10_other_occupancies_bit_exact(device_scenes, oracle_scenes, occ):
+    """Variant 10 at 5 and 7 waves/SIMD (the default is 6) renders the oracle's frame bit for bit too."""
+    _, ref = device_scenes["cornell_bunny"]
+    w, h, spp = 96, 64, 64
+    r = crt_amd.Renderer(w, h)
+    cam = crt_amd.camera(spp)
+    r.set_camera(cam)
+    r.set_kernel_variant(10)
+    r.set_occupancy_target(occ)
+    r.init_rand(41)
+    r.render(ref, spp, 20)
+    r.synchronize()
+    assert r.last_kernel_name() == f"crt_render_kernel<false, 10, {occ}>"
+    o_sum, _, o_cnt = oracle_scenes["cornell_bunny"].render(crt_amd.camera_floats(cam), w, h, spp, 20)
+    assert np.array_equal(r.linear().view(np.uint32), o_sum.view(np.uint32))
     assert r.counters()["rays"] == o_cnt["rays"]
