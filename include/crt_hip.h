@@ -279,7 +279,7 @@ int  crt_renderer_set_pixel_shard(crt_renderer* r, int shard, int shards);
 int  crt_renderer_set_stack_lds(crt_renderer* r, int entries);
 /* Register-allocation occupancy target in waves per SIMD (1 = compiler default, 4-8; 0 = auto, the default: 7 for
  * variant 8 when the frame has at least 4 of its 8x8 tiles per wave slot, 6 for the other 4-wide launches and for
- * variant 10, 5 for variants 0-3).  The 4-wide kernels keep 12 traversal-stack
+ * variants 3 and 10, 5 for variants 0-2).  The 4-wide kernels keep 12 traversal-stack
  * entries per lane in LDS at 6 waves and 8 at 7+ (LDS is allocated in 1-KiB steps per workgroup). */
 int  crt_renderer_set_occupancy_target(crt_renderer* r, int waves_per_simd);
 /* Trace `spp` samples per pixel continuing each pixel's RNG stream; the per-pixel

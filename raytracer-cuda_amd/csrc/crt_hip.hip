@@ -2614,7 +2614,7 @@ struct crt_renderer {
     int crit_threshold = 16;       // (measured: profiles/r02h, r02i)
     int top_levels = -1;           // 4-wide variants: new rays' first node steps from LDS; -1 = CRT_TOP_LEVELS
     int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 7 for variant 8 over >= 4 tiles per wave
-                                   // slot, 6 for the other 4-wide launches and variant 10, 5 for variants 0-3
+                                   // slot, 6 for the other 4-wide launches and variants 3 and 10, 5 for variants 0-2
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
     size_t ovf_entries = 0;
     int stack_lds = STACK_LDS;     // variant 4: per-lane stack entries kept in LDS
@@ -3145,8 +3145,8 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     // else at 6: a frame with few tiles per slot ends with its most expensive tile's sequential sample chain, which a
     // seventh wave per SIMD slows down (config B, 2 tiles per slot: +3.3 % at 7, profiles/r03ak).  The other 4-wide
     // variants run at 6, threaded scenes at 5.
-    // Variant 10 (threaded, bit-exact) runs at 6 (80 VGPRs; -8.0 % against 5, profiles/r03am).
-    int occ = R->min_waves ? R->min_waves : (S->width == 4 ? 6 : tv == 10 ? 6 : 5);
+    // Variants 10 and 3 (threaded, bit-exact) run at 6 (80 VGPRs; -8.0 % and -4.8 % against 5, profiles/r03am, r03as).
+    int occ = R->min_waves ? R->min_waves : (S->width == 4 || tv == 10 || tv == 3 ? 6 : 5);
     if (!R->min_waves && S->width == 4 && (wv == 8 || R->tile_shards > 1)) {
         if (!R->n_cus) HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
         const size_t tiles = (size_t)((R->width + 7) / 8) * ((R->height + 7) / 8) / (size_t)std::max(1, R->tile_shards);
@@ -3361,7 +3361,8 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     else if (tv == 0) CRT_LAUNCH(0, 1);
     else if (tv == 1) CRT_LAUNCH(1, 1);
     else if (tv == 3) {
-        if (occ >= 5) CRT_LAUNCH(3, 5);
+        if (occ >= 6) CRT_LAUNCH(3, 6);
+        else if (occ >= 5) CRT_LAUNCH(3, 5);
         else if (occ >= 4) CRT_LAUNCH(3, 4);
         else CRT_LAUNCH(3, 1);
     }
