@@ -117,7 +117,15 @@ def parse():
     ap.add_argument("--host-build", action="store_true",
                     help="build the BVHs on the host (mesh: the sequential restatement of the reference builder; "
                          "rebuilt tree: crt_sah.h) instead of on the GPU")
-    return ap.parse_args()
+    args = ap.parse_args()
+    # flag combinations the library would reject only at the first render, after the GPU is initialised
+    if args.shard == "pixels" and (args.bvh != "rebuilt" or args.bvh_width != 4):
+        ap.error("--shard pixels needs the 4-wide rebuilt BVH (--bvh rebuilt --bvh-width 4): it runs variant 8")
+    if args.spatial_splits and args.bvh != "rebuilt":
+        ap.error("--spatial-splits builds the rebuilt tree; it has no effect with --bvh reference")
+    if args.bvh_width not in (2, 4):
+        ap.error("--bvh-width must be 2 or 4")
+    return args
 
 
 def cgroup_cpu_quota():
@@ -223,7 +231,7 @@ def roofline_counters(key: str, kname: str):
     return e if e and e.get("kernel") == kname else None
 
 
-def roofline_from_counters(e, rays: int, kernel_s: float):
+def roofline_from_counters(e, rays: int, kernel_s: float, algorithmic_ops: int | None = None):
     """Utilisation of the units that can bind the render kernel, from the per-ray counter values of the committed
     PMC run (same workload, same kernel) scaled by THIS run's exact ray count and HIP-event kernel time.  The bound is
     the unit with the largest fraction of its peak (MI355X_MICROARCH.md chip table: 1024 SIMDs at 2.4 GHz, a wave64
@@ -236,6 +244,15 @@ def roofline_from_counters(e, rays: int, kernel_s: float):
     units["valu"] = {"achieved": round(valu, 3), "peak": round(valu_peak, 2), "unit": "TOP/s (issued lane-ops)",
                      "frac": round(valu / valu_peak, 4), "lane_util": d.get("valu_lane_util"),
                      "useful_TOP_s": round(valu * d.get("valu_lane_util", 1.0), 3)}
+    if algorithmic_ops:
+        # SURVEY §8(d)'s algorithmic f32 operations (counted exactly by the COUNT kernel) over the same kernel time,
+        # against the same non-FMA-doubled issue peak: the fraction of the VALU that does the path's own arithmetic.
+        # issued_over_algorithmic = issued lane-ops per algorithmic op (lane fill x bookkeeping instructions).
+        alg = algorithmic_ops / kernel_s / 1e12
+        units["algorithmic"] = {"achieved": round(alg, 3), "peak": round(valu_peak, 2),
+                                "unit": "TOP/s (SURVEY §8(d) f32 ops: 24*box + 54*tri + 30*sphere + 100*ray)",
+                                "frac": round(alg / valu_peak, 4),
+                                "issued_over_algorithmic": round(valu / alg, 3)}
     if "TCP_TOTAL_CACHE_ACCESSES" in pr and "vl1_calibration" in e:
         acc = pr["TCP_TOTAL_CACHE_ACCESSES"] * rays / kernel_s / 1e12
         cal = e["vl1_calibration"]
@@ -248,7 +265,7 @@ def roofline_from_counters(e, rays: int, kernel_s: float):
     if "hbm_bytes_per_launch" in d:
         hbm = d["hbm_bytes_per_launch"] / e["rays_per_launch"] * rays / kernel_s / 1e9
         units["hbm"] = {"achieved": round(hbm, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(hbm / HBM_PEAK_GBS, 5)}
-    bound = max(units, key=lambda k: units[k]["frac"])
+    bound = max((k for k in units if k != "algorithmic"), key=lambda k: units[k]["frac"])
     u = units[bound]
     traffic = (d["hbm_bytes_per_launch"] / e["rays_per_launch"] * rays) if "hbm_bytes_per_launch" in d else None
     return {"bound": bound, "achieved": u["achieved"], "peak": u["peak"], "unit": u["unit"], "frac": u["frac"],
@@ -277,26 +294,31 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     local = local % max(1, torch.cuda.device_count())   # rehearsal: several ranks may share one GPU (gloo)
     torch.cuda.set_device(local)
-    if world > 1:
+    # a process group whenever torch.distributed.run launched us, even with one rank: `--nproc-per-node 1` then runs
+    # the production collective path (RCCL reduce of the framebuffer on a one-rank communicator) on a single GPU
+    launched = "TORCHELASTIC_RUN_ID" in os.environ or "MASTER_ADDR" in os.environ
+    grouped = world > 1 or launched
+    if grouped:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
             dist.init_process_group(args.dist_backend)
+        log(f"[dist] rank {rank}/{world}: backend {dist.get_backend()}")
     log_r = log if rank == 0 else (lambda *a: None)
 
     def barrier():
-        if world > 1:
+        if grouped:
             dist.barrier()
 
     def allreduce_max(x: float) -> float:
-        if world == 1:
+        if not grouped:
             return x
         t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     def allreduce_sum_i(xs):
-        if world == 1:
+        if not grouped:
             return list(xs)
         t = torch.tensor(list(xs), dtype=torch.int64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -323,8 +345,8 @@ def main():
     counts = hs.counts()
     setup = {"load_build_upload_s": round(t_scene, 3), "load_and_mesh_bvh_s": round(t_load, 3),
              "mesh_bvh_build": "host" if args.host_build else "gpu (crt_build_mesh_bvh)",
-             "rebuilt_bvh_build": ("host (SBVH)" if args.spatial_splits else "host" if args.host_build
-                                   else "gpu (binned SAH, crt_scene_options.gpu_build)"),
+             "rebuilt_bvh_build": (None if args.bvh != "rebuilt" else "host (SBVH)" if args.spatial_splits
+                                  else "host" if args.host_build else "gpu (binned SAH, crt_scene_options.gpu_build)"),
              "mesh_bvh_device_ms": round(hs.device_build_ms(), 2)}
     log_r(f"[scene] {args.scene}: {counts['n_indices'] // 3} triangles, {st['device_nodes']} nodes, "
           f"{st['device_bytes'] / 1e6:.1f} MB in HBM, load+build+upload {t_scene:.2f}s {setup}")
@@ -342,7 +364,8 @@ def main():
     if args.critical_tiles is not None:
         r.set_critical_tiles(args.critical_tiles, args.critical_lanes)
     r.set_camera(cam)
-    fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard)
+    fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard,
+                              collective=grouped)
     log_r(f"[plan] {world} rank(s), spp per rank {[fr.spp] if world == 1 else 'spp/N'}")
 
     for i in range(args.warmup):
@@ -367,6 +390,10 @@ def main():
     rays_rank = r.counters()["rays"]
     kname = r.last_kernel_name()      # the instantiation the timed frames ran (rocprofv3's spelling)
     phases = r.last_timings()         # the last timed frame: probe + tile sort, and the main render kernel alone
+    # every timed frame's phases (the renderer keeps the last 32 frames' HIP events): the roofline divides by the
+    # main kernel's average over the timed frames, the same quantity rocprofv3's average duration measures
+    hist = [r.timing_history(k) for k in range(min(args.steps, 32))]
+    phases_avg = {k: sum(h[k] for h in hist) / len(hist) for k in hist[0]}
     [rays_frame] = allreduce_sum_i([rays_rank])
     log_r(f"[timed] {args.steps} frames in {elapsed:.3f}s; render kernel {kernel_ms_avg:.1f} ms avg (rank 0); "
           f"{rays_frame} rays/frame")
@@ -397,10 +424,13 @@ def main():
                         + B_RAY * work["rays"] + B_PIXEL * W * H)
         flops_launch = (F_BOX * work["box_tests"] + F_TRI * work["tri_tests"] + F_SPHERE * work["sphere_tests"]
                         + F_RAY * work["rays"])
+        main_s = phases_avg["main_kernel_ms"] / 1e3
         algorithmic = {"bytes_per_launch": int(bytes_launch),
-                       "cache_served_GB_s": round(bytes_launch / (kernel_ms_avg / 1e3) / 1e9, 1),
+                       "cache_served_GB_s": round(bytes_launch / main_s / 1e9, 1),
                        "ops_per_launch": int(flops_launch),
-                       "ops_TOP_s": round(flops_launch / (kernel_ms_avg / 1e3) / 1e12, 3),
+                       "ops_TOP_s": round(flops_launch / main_s / 1e12, 3),
+                       "denominator": "main render kernel's HIP-event time, average over the timed frames (the "
+                                      "roofline's)",
                        "per_ray": {"box_tests": round(work["box_tests"] / work["rays"], 3),
                                    "tri_tests": round(work["tri_tests"] / work["rays"], 3),
                                    "sphere_tests": round(work["sphere_tests"] / work["rays"], 3)},
@@ -411,9 +441,11 @@ def main():
     if ec is not None:
         # the counters are the main render kernel's alone, so they are divided by its own time (HIP events around that
         # launch only), not by the whole render's, which includes the cost probe and the tile sort
-        roofline = roofline_from_counters(ec, rays_rank, phases["main_kernel_ms"] / 1e3)
-        roofline.update(kernel=kname, kernel_ms=round(phases["main_kernel_ms"], 3),
-                        kernel_ms_note="HIP events around the main render launch of the last timed frame")
+        roofline = roofline_from_counters(ec, rays_rank, phases_avg["main_kernel_ms"] / 1e3,
+                                          algorithmic["ops_per_launch"] if algorithmic else None)
+        roofline.update(kernel=kname, kernel_ms=round(phases_avg["main_kernel_ms"], 3),
+                        kernel_ms_note=f"HIP events around the main render launch, average of the {len(hist)} timed "
+                                       "frames (probe and tile sort excluded)")
     else:
         log_r(f"[roofline] no committed counter summary for {workload_key(args, fr.spp)} / {kname}: roofline null")
 
@@ -464,17 +496,19 @@ def main():
                        "triangles": counts["n_indices"] // 3, "bvh": bvh_desc, "kernel_variant": variant,
                        "parallelism": f"{args.shard}-shard x{world}" + ((" + RCCL reduce of fp32 framebuffer" if args.dist_backend == "nccl"
                                                                   else f" + {args.dist_backend} reduce (rehearsal)")
-                                                                 if world > 1 else "")},
+                                                                 if grouped else ""),
+                       "dist_backend": dist.get_backend() if grouped else None},
             "frame_wall_s": round(ms_per_step / 1e3, 4),
             "rays_per_frame": rays_frame,
             "paths_per_s": round(W * H * args.spp * args.steps / elapsed, 1),
             "render_kernel_ms_avg": round(kernel_ms_avg, 3), "render_kernel_ms_max_over_ranks": round(kernel_ms_max, 3),
             "render_phases_ms_last_frame": {k: round(v, 3) for k, v in phases.items()},
+            "render_phases_ms_avg": {k: round(v, 3) for k, v in phases_avg.items()},
             "roofline": roofline, "algorithmic": algorithmic, "cpu_baseline": cpu, "parity": parity,
             "setup": setup,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

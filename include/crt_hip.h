@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CRT_ABI_VERSION 2
+#define CRT_ABI_VERSION 3
 
 enum crt_status {
     CRT_OK = 0,
@@ -269,8 +269,9 @@ int  crt_renderer_set_critical_tiles(crt_renderer* r, int tiles, int lanes);
  * child takes that node through the regular step). */
 int  crt_renderer_set_top_levels(crt_renderer* r, int levels);
 /* Pixel sharding, the bit-exact multi-GPU mode: renders of this renderer draw only shard `shard` of
- * `shards` -- every shards-th 8x8 tile of the cost order (or of row order without the probe) -- with all samples, and
- * leave every other pixel of the linear framebuffer at 0.  Summing the shards' framebuffers (the same reduce as spp
+ * `shards` -- the 8x8 tiles whose row-order index t has t % shards == shard, dispatched most expensive first when the
+ * cost probe runs (row order without it) -- with all samples, and leave every other pixel of the linear framebuffer
+ * at 0.  Summing the shards' framebuffers (the same reduce as spp
  * sharding, every rank with subsequence base 0) gives the unsharded frame bit for bit.  4-wide rebuilt scenes only
  * (variant 8); no CRT_RENDER_ACCUMULATE.  (0, 1) = unsharded, the default. */
 int  crt_renderer_set_pixel_shard(crt_renderer* r, int shard, int shards);
@@ -317,6 +318,11 @@ float crt_renderer_last_kernel_ms(crt_renderer* r);
  * runs before the main render kernel (variant 8 / 7: the cost probe and the tile sort; 0 otherwise), out[2] = the main
  * render kernel alone. */
 int crt_renderer_last_timings(crt_renderer* r, float out[3]);
+/* The same three times for an earlier render: back = 0 is the last render, 1 the one before, up to
+ * CRT_TIMING_RING - 1.  A caller that enqueues K frames without synchronising reads every frame's main-kernel time
+ * afterwards (bench.py averages them for the roofline).  CRT_ERR_INVALID_ARGUMENT when fewer renders exist. */
+#define CRT_TIMING_RING 32
+int crt_renderer_timing_history(crt_renderer* r, int back, float out[3]);
 /* Template instantiation of the last render-kernel launch as rocprofv3 names it, e.g.
  * "crt_render_kernel<false, 4, 6>" (empty before the first launch and for variant 5). */
 const char* crt_renderer_last_kernel_name(const crt_renderer* r);

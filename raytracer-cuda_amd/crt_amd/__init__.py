@@ -309,6 +309,12 @@ class Renderer:
         check(_lib.hip().crt_renderer_last_timings(self.h, a), "last_timings")
         return {"render_ms": float(a[0]), "probe_sort_ms": float(a[1]), "main_kernel_ms": float(a[2])}
 
+    def timing_history(self, back: int) -> dict:
+        """last_timings() of an earlier render: back = 0 is the last one, up to 31 (crt_renderer_timing_history)."""
+        a = (C.c_float * 3)()
+        check(_lib.hip().crt_renderer_timing_history(self.h, int(back), a), "timing_history")
+        return {"render_ms": float(a[0]), "probe_sort_ms": float(a[1]), "main_kernel_ms": float(a[2])}
+
     def last_kernel_ms(self) -> float:
         return float(_lib.hip().crt_renderer_last_kernel_ms(self.h))
 

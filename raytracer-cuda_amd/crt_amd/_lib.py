@@ -85,7 +85,7 @@ class SceneOptions(C.Structure):
 
 BVH_REFERENCE = 0
 BVH_REBUILT = 1
-ABI_VERSION = 2          # include/crt_hip.h CRT_ABI_VERSION
+ABI_VERSION = 3          # include/crt_hip.h CRT_ABI_VERSION
 BUILD_CHECKED = 1        # crt_build_flags(): the -DCRT_CHECKED build
 
 
@@ -103,7 +103,7 @@ HIP_SYMBOLS = [
     "crt_renderer_synchronize", "crt_renderer_read_linear", "crt_renderer_read_rgba8", "crt_renderer_read_rng",
     "crt_renderer_write_linear", "crt_renderer_get_counters", "crt_renderer_linear_device_ptr",
     "crt_renderer_rgba_device_ptr", "crt_renderer_rng_device_ptr", "crt_renderer_last_kernel_ms",
-    "crt_renderer_last_kernel_name", "crt_renderer_last_timings",
+    "crt_renderer_last_kernel_name", "crt_renderer_last_timings", "crt_renderer_timing_history",
     "crt_renderer_attach_linear", "crt_renderer_set_kernel_variant", "crt_renderer_get_schedule_stats",
     "crt_renderer_set_regen_threshold", "crt_renderer_set_occupancy_target",
     "crt_build_mesh_bvh", "crt_renderer_set_schedule", "crt_renderer_set_critical_tiles", "crt_renderer_set_pixel_shard",
@@ -162,6 +162,7 @@ def hip():
             "crt_renderer_resolve": ([P, f32, P], i32), "crt_renderer_render_frame": ([P, P, P], i32),
             "crt_renderer_set_pixel_shard": ([P, i32, i32], i32),
             "crt_renderer_synchronize": ([P, P], i32), "crt_renderer_last_timings": ([P, P], i32),
+            "crt_renderer_timing_history": ([P, i32, P], i32),
             "crt_renderer_read_linear": ([P, P], i32), "crt_renderer_read_rgba8": ([P, P], i32),
             "crt_renderer_read_rng": ([P, P], i32), "crt_renderer_write_linear": ([P, P], i32),
             "crt_renderer_get_counters": ([P, P], i32),
@@ -186,14 +187,16 @@ def hip():
             "crt_selftest_sqrt": ([C.c_uint32, C.c_uint32, P, P], i32),
         }
         for name, (args, res) in sig.items():
-            if os.environ.get("CRT_HIP_LIB") and not hasattr(L, name):
+            if os.environ.get("CRT_SKIP_ABI_CHECK") and not hasattr(L, name):
                 continue   # an A/B build of an older revision: self-tests added since then are absent
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
-        if L.crt_abi_version() != ABI_VERSION and not os.environ.get("CRT_HIP_LIB"):
+        # every library is checked, CRT_HIP_LIB overrides included (a stale build would silently misread newer
+        # fields); A/B runs against an older revision's build opt out explicitly with CRT_SKIP_ABI_CHECK=1
+        if L.crt_abi_version() != ABI_VERSION and not os.environ.get("CRT_SKIP_ABI_CHECK"):
             raise CrtError(f"{HIP_LIB}: C ABI version {L.crt_abi_version()}, these bindings expect {ABI_VERSION} "
-                           "(rebuild the library)")
+                           "(rebuild the library, or set CRT_SKIP_ABI_CHECK=1 for an A/B run of an older build)")
         _hip = L
     return _hip
 

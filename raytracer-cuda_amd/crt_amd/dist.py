@@ -54,7 +54,7 @@ class ShardedFrameRenderer:
 
     def __init__(self, renderer, scene, spp_total: int, max_bounces: int = 20, seed: int = 41,
                  rank: int = 0, world: int = 1, group=None, reduce_op: str = "reduce", fb_device=None,
-                 mode: str = "spp"):
+                 mode: str = "spp", collective: bool | None = None):
         if mode not in ("spp", "pixels"):
             raise ValueError("mode must be 'spp' or 'pixels'")
         self.mode = mode
@@ -67,6 +67,14 @@ class ShardedFrameRenderer:
         self.seed = int(seed)
         self.rank, self.world, self.group = rank, world, group
         self.reduce_op = reduce_op
+        # the collective runs for every world > 1 and, when asked (or a process group exists), for one rank too: the
+        # production RCCL path on a one-rank communicator (bench.py under torch.distributed.run --nproc-per-node 1)
+        if collective is None:
+            import torch.distributed as dist
+            collective = world > 1 or (dist.is_available() and dist.is_initialized())
+        if world > 1 and not collective:
+            raise ValueError("world > 1 needs the framebuffer collective")
+        self.collective = bool(collective)
         if mode == "spp":
             self.spp = shard_spp(spp_total, world, rank)
             self.subseq = subsequence_base(rank, renderer.width, renderer.height)
@@ -94,7 +102,7 @@ class ShardedFrameRenderer:
         self.r.render(self.scene, self.spp, self.max_bounces, stream=st)
         if ev_end is not None:
             ev_end.record()
-        if self.world > 1:
+        if self.collective:
             import torch.distributed as dist
             if self.reduce_op == "all_reduce":
                 dist.all_reduce(self.fb, op=dist.ReduceOp.SUM, group=self.group)

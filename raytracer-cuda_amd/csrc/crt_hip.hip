@@ -2586,9 +2586,14 @@ struct crt_renderer {
     unsigned long long* d_counters = nullptr;
     crt_camera_desc cam{};
     bool has_camera = false;
+    // HIP events of the current render: ev0 before the cost probe, ev_main just before the main render kernel (after
+    // the probe and the tile sort), ev1 after it.  They point into a ring of CRT_TIMING_RING frames, so a caller that
+    // renders K frames back to back without synchronising can read every frame's phases afterwards
+    // (crt_renderer_timing_history).
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    hipEvent_t ev_main = nullptr;  // recorded just before the main render kernel (after the cost probe and tile sort)
-    bool timed = false;
+    hipEvent_t ev_main = nullptr;
+    hipEvent_t ring[CRT_TIMING_RING][3] = {};
+    unsigned long long n_timed = 0;   // renders whose three events were all recorded
     char kernel_name[64] = "";     // instantiation of the last render launch, rocprof's spelling
     // variant 7: pixel order, slot queue, probe costs, sort scratch (allocated on first use)
     uint32_t* d_order = nullptr;
@@ -2912,6 +2917,13 @@ int crt_selftest_uv_div(int dim, unsigned long long* mismatches) {
     return uv_div_mismatches(dim, mismatches);
 }
 
+static hipError_t create_timing_ring(crt_renderer* R) {
+    for (auto& slot : R->ring)
+        for (hipEvent_t& ev : slot)
+            if (hipError_t e = hipEventCreate(&ev); e != hipSuccess) return e;
+    return hipSuccess;
+}
+
 int crt_renderer_create(int width, int height, int device, crt_renderer** out) {
     if (!out || width <= 0 || height <= 0 || (long long)width * height > (1LL << 31) / 6)
         return set_error(CRT_ERR_INVALID_ARGUMENT, "bad renderer size");
@@ -2932,8 +2944,7 @@ int crt_renderer_create(int width, int height, int device, crt_renderer** out) {
         (e = hipMemset(R->d_sum_own, 0, n * 3 * 4)) != hipSuccess ||
         (e = hipMemset(R->d_rgba, 0, n * 4)) != hipSuccess ||
         (e = hipMemset(R->d_counters, 0, 16 * sizeof(unsigned long long))) != hipSuccess ||
-        (e = hipEventCreate(&R->ev0)) != hipSuccess || (e = hipEventCreate(&R->ev1)) != hipSuccess ||
-        (e = hipEventCreate(&R->ev_main)) != hipSuccess) {
+        (e = create_timing_ring(R)) != hipSuccess) {
         crt_renderer_destroy(R);
         return set_error(e == hipErrorOutOfMemory ? CRT_ERR_OUT_OF_MEMORY : CRT_ERR_HIP,
                          std::string("renderer allocation: ") + hipGetErrorString(e));
@@ -2981,9 +2992,9 @@ void crt_renderer_destroy(crt_renderer* R) {
     if (R->d_order_hist) (void)hipFree(R->d_order_hist);
     if (R->d_tile_key) (void)hipFree(R->d_tile_key);
     if (R->d_rng_cache) (void)hipFree(R->d_rng_cache);
-    if (R->ev0) (void)hipEventDestroy(R->ev0);
-    if (R->ev1) (void)hipEventDestroy(R->ev1);
-    if (R->ev_main) (void)hipEventDestroy(R->ev_main);
+    for (auto& slot : R->ring)
+        for (hipEvent_t& ev : slot)
+            if (ev) (void)hipEventDestroy(ev);
     delete R;
 }
 
@@ -3121,6 +3132,20 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     dim3 grid((R->width + 15) / 16, (R->height + 15) / 16), block(256);
     const bool cnt = (flags & CRT_RENDER_COUNT_WORK) != 0;
     P.regen_threshold = S->width == 4 ? R->regen_threshold_wide : R->regen_threshold;
+    if (R->tile_shards > 1) {
+        // pixel sharding: variant 8 renders this shard's tiles; every other pixel of the framebuffer is 0, so the sum
+        // of the shards' framebuffers (one collective) is the unsharded frame exactly (x + 0 = x).  Checked and
+        // cleared before ev0, so a rejected call leaves the previous frame's timings intact and the clear is not
+        // counted as probe/sort time.
+        if (S->width != 4) return set_error(CRT_ERR_UNSUPPORTED, "pixel sharding needs a 4-wide rebuilt scene (variant 8)");
+        if (P.accumulate) return set_error(CRT_ERR_INVALID_ARGUMENT, "pixel sharding does not accumulate");
+        HIP_TRY(hipMemsetAsync(R->d_sum, 0, (size_t)R->width * R->height * 3 * sizeof(float), st));
+    }
+    {   // this render's slot of the timing ring: the oldest frame's, so a render that fails half-way never touches
+        // the slot of the last complete frame
+        hipEvent_t* slot = R->ring[R->n_timed % CRT_TIMING_RING];
+        R->ev0 = slot[0]; R->ev_main = slot[1]; R->ev1 = slot[2];
+    }
     HIP_TRY(hipEventRecord(R->ev0, st));
 #define CRT_LAUNCH(V, W)                                                                     \
     do {                                                                                     \
@@ -3169,14 +3194,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         }
         P.ovf = R->d_ovf;
     }
-    if (R->tile_shards > 1) {
-        // pixel sharding: variant 8 renders this shard's tiles; every other pixel of the framebuffer is 0, so the sum
-        // of the shards' framebuffers (one collective) is the unsharded frame exactly (x + 0 = x)
-        if (S->width != 4) return set_error(CRT_ERR_UNSUPPORTED, "pixel sharding needs a 4-wide rebuilt scene (variant 8)");
-        if (P.accumulate) return set_error(CRT_ERR_INVALID_ARGUMENT, "pixel sharding does not accumulate");
-        wv = 8;
-        HIP_TRY(hipMemsetAsync(R->d_sum, 0, (size_t)R->width * R->height * 3 * sizeof(float), st));
-    }
+    if (R->tile_shards > 1) wv = 8;   // pixel sharding (checked above)
     if (S->width == 4 && wv == 8) {
         const size_t n_pix = (size_t)R->width * R->height;
         const int tiles_x = (R->width + 7) / 8, n_tiles = tiles_x * ((R->height + 7) / 8);
@@ -3373,7 +3391,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
 #undef CRT_LAUNCH
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(R->ev1, st));
-    R->timed = true;
+    ++R->n_timed;
     return CRT_OK;
 }
 
@@ -3549,23 +3567,29 @@ extern "C" int crt_profile_wave_times(unsigned long long* out, int n_waves) {
 }
 #endif
 
-int crt_renderer_last_timings(crt_renderer* R, float out[3]) {
+int crt_renderer_timing_history(crt_renderer* R, int back, float out[3]) {
     if (!R || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
-    if (!R->timed) return set_error(CRT_ERR_INVALID_ARGUMENT, "no render yet");
+    if (back < 0 || back >= CRT_TIMING_RING) return set_error(CRT_ERR_INVALID_ARGUMENT, "back outside [0, CRT_TIMING_RING)");
+    if ((unsigned long long)back >= R->n_timed) return set_error(CRT_ERR_INVALID_ARGUMENT, "fewer renders than back + 1");
+    hipEvent_t* slot = R->ring[(R->n_timed - 1 - (unsigned long long)back) % CRT_TIMING_RING];
     HIP_TRY(hipSetDevice(R->device));
-    HIP_TRY(hipEventSynchronize(R->ev1));
-    HIP_TRY(hipEventElapsedTime(&out[0], R->ev0, R->ev1));
-    HIP_TRY(hipEventElapsedTime(&out[1], R->ev0, R->ev_main));
-    HIP_TRY(hipEventElapsedTime(&out[2], R->ev_main, R->ev1));
+    HIP_TRY(hipEventSynchronize(slot[2]));
+    HIP_TRY(hipEventElapsedTime(&out[0], slot[0], slot[2]));
+    HIP_TRY(hipEventElapsedTime(&out[1], slot[0], slot[1]));
+    HIP_TRY(hipEventElapsedTime(&out[2], slot[1], slot[2]));
     return CRT_OK;
 }
 
+int crt_renderer_last_timings(crt_renderer* R, float out[3]) {
+    if (!R || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    if (!R->n_timed) return set_error(CRT_ERR_INVALID_ARGUMENT, "no render yet");
+    return crt_renderer_timing_history(R, 0, out);
+}
+
 float crt_renderer_last_kernel_ms(crt_renderer* R) {
-    if (!R || !R->timed) return -1.f;
-    if (hipSetDevice(R->device) != hipSuccess || hipEventSynchronize(R->ev1) != hipSuccess) return -1.f;
-    float ms = -1.f;
-    if (hipEventElapsedTime(&ms, R->ev0, R->ev1) != hipSuccess) return -1.f;
-    return ms;
+    float t[3];
+    if (!R || !R->n_timed || crt_renderer_timing_history(R, 0, t) != CRT_OK) return -1.f;
+    return t[0];
 }
 
 int crt_selftest_math(const float* a, const float* b, int n, float* out, double* out64) {

@@ -41,7 +41,7 @@ def test_host_library_exports_header():
 def test_libraries_load_without_gpu():
     from crt_amd import _lib
     L = _lib.hip()
-    assert L.crt_abi_version() == 2
+    assert L.crt_abi_version() == 3
     n = C.c_int(-1)
     assert L.crt_device_count(C.byref(n)) == 0 and n.value >= 0
     _lib.host()
@@ -51,6 +51,7 @@ def test_timings_need_a_render():
     from crt_amd import _lib
     ms = (C.c_float * 3)()
     assert _lib.hip().crt_renderer_last_timings(None, ms) == -1
+    assert _lib.hip().crt_renderer_timing_history(None, 0, ms) == -1
     assert _lib.hip().crt_build_flags() == 0
 
 

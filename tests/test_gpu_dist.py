@@ -1,7 +1,7 @@
 """The spp-sharded multi-GPU path with the real HIP kernel (crt_amd/dist.py), 2 and 3 ranks.
 
 No 8-GPU node is available to this build, so the ranks share cuda:0 over the gloo backend (RCCL refuses two ranks on
-one GPU).  Everything else is the production path: each rank's kernel writes its shard's fp32 sums into a torch
+one GPU); RCCL itself runs on a one-rank communicator (test_rccl_one_rank_equals_the_unsharded_frame).  Everything else is the production path: each rank's kernel writes its shard's fp32 sums into a torch
 tensor, `reduce` / `all_reduce` sums them, rank 0 resolves with 1/spp_total.  Checked against the same shards rendered
 one after another in this process and summed on the host: with 2 ranks bit for bit (fp32 a + b is commutative); with 3
 to within one rounding of the sum order.  The resolved RGBA8 is writeColor of the reduced sums.
@@ -32,11 +32,11 @@ def _port():
     return p
 
 
-def _run(tmp_path, world, reduce_op, spp=SPP, mode="spp"):
-    out = str(tmp_path / f"frame_{world}_{reduce_op}_{mode}")
+def _run(tmp_path, world, reduce_op, spp=SPP, mode="spp", backend="gloo"):
+    out = str(tmp_path / f"frame_{world}_{reduce_op}_{mode}_{backend}")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", str(REPO / "tests" / "helpers" / "dist_frame_worker.py"),
-           out, str(W), str(H), str(spp), reduce_op, mode]
+           out, str(W), str(H), str(spp), reduce_op, mode, backend]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="2"))
     assert p.returncode == 0, p.stderr[-4000:]
     return out
@@ -70,6 +70,29 @@ def test_two_ranks_equal_the_summed_shards(tmp_path, reduce_op):
     if reduce_op == "all_reduce":
         other = np.load(out + ".rank1.npz")
         assert np.array_equal(other["lin"].view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("reduce_op", ["reduce", "all_reduce"])
+def test_rccl_one_rank_equals_the_unsharded_frame(tmp_path, reduce_op):
+    """The production collective through RCCL itself: torch.distributed.run --nproc-per-node 1 with backend nccl (a
+    one-rank communicator; RCCL refuses two ranks on one GPU, and the 8-GPU node is the driver's).  The worker's frame
+    went through ShardedFrameRenderer's dist.reduce / all_reduce on the fp32 framebuffer the HIP kernel wrote; it must
+    equal the unsharded 1-GPU frame bit for bit, sums and RGBA8."""
+    out = _run(tmp_path, 1, reduce_op, backend="nccl")
+    got = np.load(out + ".rank0.npz")
+    assert str(got["backend"]) == "nccl" and int(got["world"]) == 1
+    assert int(got["spp"]) == SPP and int(got["subseq"]) == 0
+    hs = crt_amd.HostScene(assets.scene_files("cornell_bunny"))
+    sc = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
+    r = crt_amd.Renderer(W, H, 0)
+    r.set_camera(crt_amd.camera(SPP))
+    r.init_rand(41)
+    r.render(sc, SPP, 20)
+    r.resolve(crt_amd.pixel_sample_scale(SPP))
+    r.synchronize()
+    assert np.array_equal(got["lin"].view(np.uint32), r.linear().view(np.uint32))
+    assert np.array_equal(got["rgba"], r.rgba8())
+    assert int(got["rays"]) == r.counters()["rays"]
 
 
 def test_three_ranks_uneven_spp(tmp_path):

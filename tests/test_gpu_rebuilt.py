@@ -283,3 +283,49 @@ def test_occupancy_seven_is_bit_identical_and_automatic(rebuilt):
     assert np.array_equal(lin6, lin7) and np.array_equal(rng6, rng7) and rays6 == rays7
     small = _frame(dev, 104, 45, 64, 20, crt_amd.camera(64), variant=-1)
     assert small.last_kernel_name() == "crt_render_kernel<false, 8, 6>"
+
+
+def _usable_cores() -> int:
+    """The affinity set capped by the cgroup CPU quota (the GPU box: 256 CPUs, a 16-CPU quota)."""
+    import os
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def test_shipped_instantiation_against_the_oracle(rebuilt, oracle_scenes):
+    """The benchmarked kernel itself against the oracle, with no GPU-vs-GPU link in between: a headline-sized frame
+    (2560x1440, so >= 4 tiles per wave slot) at 64 spp through the automatic choice, which runs the cost probe, the tile
+    sort and the critical tiles and launches crt_render_kernel<false, 8, 7>.  Four full-width bands, one through the
+    glass bunny, are rendered by the oracle (CUDAKernels.h:147-166 restated) from the same RNG streams; each band holds
+    the north-star bar (per-channel RMS <= 1e-4) with >= 99.9 % of its pixels bit-identical."""
+    dev = rebuilt["cornell_bunny", "w4"]
+    w, h, spp = 2560, 1440, 64
+    cam = crt_amd.camera(spp)
+    r = crt_amd.Renderer(w, h)
+    r.set_camera(cam)
+    r.init_rand(41)
+    r.render(dev, spp, 20)
+    r.resolve(crt_amd.pixel_sample_scale(spp))
+    r.synchronize()
+    assert r.last_kernel_name() == "crt_render_kernel<false, 8, 7>"
+    ph = r.last_timings()
+    assert ph["probe_sort_ms"] > 0 and ph["main_kernel_ms"] > 0          # the probe and the sort ran before the kernel
+    lin, rgba = r.linear(), r.rgba8()
+    cf = crt_amd.camera_floats(cam)
+    nt = _usable_cores()
+    osc = oracle_scenes["cornell_bunny"]
+    per_sample = {}
+    for y0 in (96, 700, 950, 1360):
+        o_sum, o_rgba, o_cnt = osc.render(cf, w, h, spp, 20, rect=(0, y0, w, y0 + 4), nthreads=nt)
+        _compare(lin[y0:y0 + 4], o_sum, spp, 0.999)
+        assert np.mean(np.all(rgba[y0:y0 + 4] == o_rgba, axis=-1)) >= 0.999
+        per_sample[y0] = o_cnt["rays"] / (w * 4 * spp)
+    # the y0 = 950 band crosses the glass bunny (x ~1360-1600): its paths there are the frame's longest
+    _, _, c = osc.render(cf, w, h, spp, 20, rect=(1360, 950, 1600, 954), nthreads=nt)
+    assert c["rays"] / (240 * 4 * spp) > 1.15 * per_sample[950], (c["rays"], per_sample)
