@@ -105,6 +105,8 @@ def parse():
     ap.add_argument("--critical-tiles", type=int, default=None,
                     help="variant 8: leading tiles of the cost order that regenerate sooner (default: library's)")
     ap.add_argument("--critical-lanes", type=int, default=16, help="their regeneration threshold")
+    ap.add_argument("--carry", type=int, nargs=2, default=None, metavar=("LANES", "MAX_PAIRS"),
+                    help="variant 8 leaf-pair carry (crt_renderer_set_leaf_carry; CRT_LEAF_CARRY builds)")
     ap.add_argument("--bvh", default="rebuilt", choices=["rebuilt", "reference"])
     ap.add_argument("--bvh-width", type=int, default=4, help="rebuilt BVH: 4 (variant 4) or 2 (threaded)")
     ap.add_argument("--leaf-size", type=int, default=4)
@@ -363,6 +365,8 @@ def main():
         r.set_schedule(args.probe_spp, 64)
     if args.critical_tiles is not None:
         r.set_critical_tiles(args.critical_tiles, args.critical_lanes)
+    if args.carry is not None:
+        r.set_leaf_carry(*args.carry)
     r.set_camera(cam)
     fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard,
                               collective=grouped)

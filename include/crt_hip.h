@@ -268,6 +268,10 @@ int  crt_renderer_set_critical_tiles(crt_renderer* r, int tiles, int lanes);
  * order and the stack entries are the traversal's own, so results never depend on it (a ray whose step hits a leaf
  * child takes that node through the regular step). */
 int  crt_renderer_set_top_levels(crt_renderer* r, int levels);
+/* Variant 8's leaf-pair carry (kernels built with CRT_LEAF_CARRY): a traversal step runs whole rounds of 64 leaf pairs
+ * and carries a part-empty remainder of at most `max_pairs` (0..63; 0 = never) pairs to the next step when at least
+ * `lanes` (0..64; 65 = never) lanes are still traversing.  Results never depend on it. */
+int  crt_renderer_set_leaf_carry(crt_renderer* r, int lanes, int max_pairs);
 /* Pixel sharding, the bit-exact multi-GPU mode: renders of this renderer draw only shard `shard` of
  * `shards` -- the 8x8 tiles whose row-order index t has t % shards == shard, dispatched most expensive first when the
  * cost probe runs (row order without it) -- with all samples, and leave every other pixel of the linear framebuffer

@@ -79,6 +79,9 @@ struct RenderParams {
     int crit_tiles, crit_threshold;       // variant 8: the first crit_tiles tiles of the cost order regenerate at
                                           // crit_threshold parked lanes instead of regen_threshold
     int top_levels;                       // 4-wide variants: a new ray's first node steps taken from LDS (<= CRT_TOP_LEVELS)
+    int carry_lanes, carry_max;           // variant 8 leaf-pair carry (traverse_step4c): a step's part-empty round of
+                                          // at most carry_max pairs waits for the next step when at least carry_lanes
+                                          // lanes are still traversing
 };
 
 #ifdef CRT_PROFILE_PAIRS
@@ -1057,6 +1060,104 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
     if (COUNT) cnt.cyc_round += shader_clock() - c1;
 }
 
+#ifndef CRT_LEAF_CARRY
+#define CRT_LEAF_CARRY 0
+#endif
+// Variant 8's traversal step with the leaf-pair carry (CRT_LEAF_CARRY).  traverse_step4 runs every step's pairs at
+// once, so a step with 70 pairs runs a full round and one of 6 pairs.  Here a step runs only whole rounds of 64 pairs
+// and CARRIES the part-empty remainder to the next step, whose new pairs fill it up:
+//  * `pend` = (first primitive << 8) | count of the lane's untested leaf pairs (0 = none).  A lane with a carried span
+//    takes no node step, so its `closest` stays the value the span was opened with: the same box tests, the same
+//    pairs against the same tmax, hence the same traversal as traverse_step4, bit for bit and count for count.  Only
+//    the round boundaries move, and the per-owner (t, ~rank) min (Mesh.cuh:90-103 restated, see traverse_step4) does
+//    not depend on them.
+//  * carried pairs are listed before the step's new pairs (one packed DPP scan: carried counts in the high 16 bits),
+//    so they are always in the first round: a lane waits at most one step.  A remainder is carried only when the
+//    carried pairs fit the whole rounds (so none waits twice), it holds at most carry_max pairs, and at least
+//    carry_lanes lanes are still traversing (a draining wave would not fill it); otherwise the step runs it.
+//  * a lane's LDS key stays ~0 except while its span is being tested, and is reset when its span completes, so a
+//    partly tested span keeps its running min across steps.
+template <bool COUNT>
+__device__ __forceinline__ void traverse_step4c(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
+                                                float& closest, int& hit, uint32_t& pend, TraceCounts& cnt,
+                                                WaveLdsWide& L, uint32_t* __restrict__ stk, int lane, size_t pix,
+                                                size_t n_pix) {
+    if (COUNT) cnt.step_slots++;
+    const uint64_t c0 = COUNT ? shader_clock() : 0;
+    int leaf_n, leaf_first;
+    const bool carried = pend != 0u;
+    if (carried) {
+        leaf_first = (int)(pend >> 8);
+        leaf_n = (int)(pend & 0xffu);
+    } else {
+        node_step4<COUNT>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
+    }
+    const uint64_t c1 = COUNT ? shader_clock() : 0;
+    if (COUNT) cnt.cyc_step += c1 - c0;
+    if (!wave_ballot(leaf_n > 0)) return;
+    // one scan for both lists (each sum < 64 * 256 < 2^16): carried pairs first, then the step's new pairs
+    const int incl = wave_inclusive_scan_dpp(carried ? (leaf_n << 16) : leaf_n);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+    const int total_c = (int)(tot >> 16), total = total_c + (int)(tot & 0xffffu);
+    const int pfx = carried ? (incl >> 16) - leaf_n : total_c + (incl & 0xffff) - leaf_n;
+    int limit = total & ~63;                 // whole rounds (uniform)
+    const int rem = total - limit;
+    if (rem != 0 && !(limit >= total_c && rem <= P.carry_max &&
+                      __popcll(wave_ballot(node >= 0)) >= P.carry_lanes))
+        limit = total;                       // run the remainder now
+    L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first - pfx));
+#ifdef CRT_CHECKED
+    L.prefix[lane] = pfx;
+    L.span_n[lane] = leaf_n;
+#endif
+    uint32_t carry = 0;   // owner + 1 of the last pair of the previous round
+    for (int base = 0; base < limit; base += 64) {
+        if (COUNT) cnt.round_slots++;
+        if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)(lane + 1);
+        wave_sync();
+        const uint32_t mark = L.owner_at[lane];
+        L.owner_at[lane] = 0;
+        const uint32_t owner1 = max(wave_inclusive_max_scan_u(mark), carry);
+        const int owner = (int)owner1 - 1;
+        const int j = base + lane;
+        if (j < limit) {
+            const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
+            const int p = __float_as_int(r1.w) + j;
+            if (COUNT) cnt.tris++;
+            int rank;
+#ifdef CRT_CHECKED
+            const bool bad = (unsigned)owner >= 64u || j < L.prefix[owner] || j >= L.prefix[owner] + L.span_n[owner] ||
+                             (unsigned)p >= (unsigned)P.n_prims;
+            if (bad) atomicOr(P.err, 4u);
+            rank = -1;
+            const float t = bad ? -1.f : prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
+                                                   P.tree_spheres != 0);
+#else
+            const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
+                                      P.tree_spheres != 0);
+#endif
+            const unsigned long long kp = ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank);
+            atomicMin(&L.key[owner], t >= 0.f ? kp : ~0ull);
+        }
+        carry = __builtin_amdgcn_readlane(owner1, 63);
+        wave_sync();
+    }
+    {
+        const int done = min(max(limit - pfx, 0), leaf_n);    // this lane's pairs tested in this step's rounds
+        const bool fin = leaf_n > 0 && done == leaf_n;
+        const unsigned long long kk = L.key[lane];
+        const float t = __uint_as_float((unsigned)(kk >> 32));
+        const int rank = (int)(0xffffffffu - (unsigned)kk);
+        if (fin && kk != ~0ull && better(t, rank, closest, hit)) {
+            closest = t;
+            hit = rank;
+        }
+        L.key[lane] = fin ? ~0ull : kk;
+        pend = (leaf_n > 0 && !fin) ? (((uint32_t)(leaf_first + done) << 8) | (uint32_t)(leaf_n - done)) : 0u;
+    }
+    if (COUNT) cnt.cyc_round += shader_clock() - c1;
+}
+
 // The tree's top nodes held in LDS (CRT_TOP_LEVELS): the root and, at level 2, its internal children, copied once
 // per workgroup with their rows unswizzled (row k at 16-B slot k).  Every ray starts at the root, and its first node
 // steps are the same for every ray up to the direction signs, so a new ray takes them in the regeneration pass from
@@ -1563,12 +1664,16 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         V3 inv = v3(0.f, 0.f, 0.f);
         uint32_t rows = 0;         // ray_rows(inv)
         L.owner_at[lane] = 0;      // traverse_step4: owner + 1, 0 = none
+        constexpr bool CARRY = TILED && CRT_LEAF_CARRY != 0;
+        uint32_t pend = 0;         // traverse_step4c: the lane's carried leaf span, 0 = none
+        if (CARRY) L.key[lane] = ~0ull;
         // variant 8: the most expensive tiles of the cost order bound the frame when it has few tiles per wave slot
         // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
         const int regen_t = (TILED && (int)blockIdx.x < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
         bool first_pass = true;    // uniform
         for (;;) {
-            const uint64_t parked_mask = live_mask & wave_ballot(node < 0);
+            // a lane whose trace ended but whose carried leaf pairs are untested is not parked yet
+            const uint64_t parked_mask = live_mask & wave_ballot(CARRY ? (node < 0 && pend == 0u) : node < 0);
             const int n_parked = __popcll(parked_mask);
             const int n_live = __popcll(live_mask);
             if (n_live == 0) break;
@@ -1617,7 +1722,12 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 if (TILED) wave_rays += (uint32_t)__popcll(parked_mask & live_mask);
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
-            traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
+            if constexpr (CARRY)
+                traverse_step4c<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, pend, cnt, L, stk, lane,
+                                       (size_t)pix, n_pix);
+            else
+                traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix,
+                                      n_pix);
         }
     } else if constexpr (VARIANT == 2 || VARIANT == 3 || VARIANT == 10) {
         constexpr bool PF = VARIANT == 3 || VARIANT == 10;
@@ -2618,6 +2728,7 @@ struct crt_renderer {
     int tile_shard = 0, tile_shards = 1;   // pixel sharding (crt_renderer_set_pixel_shard)
     int crit_threshold = 16;       // (measured: profiles/r02h, r02i)
     int top_levels = -1;           // 4-wide variants: new rays' first node steps from LDS; -1 = CRT_TOP_LEVELS
+    int carry_lanes = 16, carry_max = 63;   // variant 8 leaf-pair carry (builds with CRT_LEAF_CARRY)
     int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 7 for variant 8 over >= 4 tiles per wave
                                    // slot, 6 for the other 4-wide launches and variants 3 and 10, 5 for variants 0-2
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
@@ -3122,6 +3233,8 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.ovf = nullptr;
     P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0; P.crit_tiles = 0; P.crit_threshold = 64;
     P.top_levels = R->top_levels < 0 ? CRT_TOP_LEVELS : R->top_levels;
+    P.carry_lanes = R->carry_lanes;
+    P.carry_max = R->carry_max;
     P.stack_cap = S->stack_cap;
     P.sphere_first = S->sphere_first;
     P.n_ray_spheres = S->n_ray_spheres;
@@ -3577,6 +3690,15 @@ int crt_renderer_timing_history(crt_renderer* R, int back, float out[3]) {
     HIP_TRY(hipEventElapsedTime(&out[0], slot[0], slot[2]));
     HIP_TRY(hipEventElapsedTime(&out[1], slot[0], slot[1]));
     HIP_TRY(hipEventElapsedTime(&out[2], slot[1], slot[2]));
+    return CRT_OK;
+}
+
+int crt_renderer_set_leaf_carry(crt_renderer* R, int lanes, int max_pairs) {
+    if (!R) return set_error(CRT_ERR_INVALID_ARGUMENT, "null renderer");
+    if (lanes < 0 || lanes > 65 || max_pairs < 0 || max_pairs > 63)
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "leaf carry: lanes in [0, 65], max_pairs in [0, 63]");
+    R->carry_lanes = lanes;
+    R->carry_max = max_pairs;
     return CRT_OK;
 }
 

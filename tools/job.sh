@@ -2,7 +2,7 @@
 # The current one-off GPU job (overwritten per job; the copy that ran is kept as profiles/<id>/job.sh).
 # r04a: round-4 first check at HEAD: GPU suite (incl. RCCL one-rank and shipped-instantiation-vs-oracle tests), smoke,
 # default bench, bench through torchrun + RCCL at one rank, per-rank shares at N = 1/2/4/8, section profile at HEAD,
-# PMC passes for configs B and E, B/E benches with parity, rocprofv3 kernel stats.
+# PMC passes for configs B and E, B/E benches with parity, rocprofv3 kernel stats; leaf-pair carry bits + A/B.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=r04a; OUT=$R/gpurun_out/$O; mkdir -p $OUT
@@ -27,4 +27,12 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
     python3 $R/bench.py --no-cpu-baseline --no-parity --steps 3 > $OUT/bench_prof.log 2>&1
 cd $R
 for f in bench bench_rccl1 B E; do echo "$f: $(tail -1 $OUT/$f.log | cut -c1-200)"; done
+# leaf-pair carry (CRT_LEAF_CARRY build, tools/build_profile_lib.sh carry -DCRT_LEAF_CARRY=1): bits, pair fill, A/B
+CL=raytracer-cuda_amd/lib_exp/carry/libcrt_hip.so
+timeout -k 10 200 python3 tools/frame_hash.py --big > $OUT/hash_intree.txt 2>&1
+CRT_HIP_LIB=$R/$CL timeout -k 10 200 python3 tools/frame_hash.py --big > $OUT/hash_carry.txt 2>&1
+cmp <(grep -v amdgpu.ids $OUT/hash_intree.txt) <(grep -v amdgpu.ids $OUT/hash_carry.txt) && echo "carry: hashes identical" || echo "carry: HASHES DIFFER"
+CRT_HIP_LIB=$R/$CL timeout -k 10 300 python3 tools/section_profile.py --spp 256 > $OUT/section_C256_carry.txt 2>&1
+bash tools/gpu_job.sh ab $O/ab $CL 3
+for f in $OUT/ab/bench_*.log; do echo "$(basename $f): $(grep -o '"main_kernel_ms": [0-9.]*' $f | tail -1)"; done
 echo job done
