@@ -1110,15 +1110,19 @@ __device__ __forceinline__ void traverse_step4c(const RenderParams& P, V3 o, V3 
     L.prefix[lane] = pfx;
     L.span_n[lane] = leaf_n;
 #endif
-    uint32_t carry = 0;   // owner + 1 of the last pair of the previous round
+    uint32_t carry = 0;   // owner of the last pair of the previous round (round 0 starts with a mark)
     for (int base = 0; base < limit; base += 64) {
         if (COUNT) cnt.round_slots++;
         if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)(lane + 1);
         wave_sync();
         const uint32_t mark = L.owner_at[lane];
         L.owner_at[lane] = 0;
-        const uint32_t owner1 = max(wave_inclusive_max_scan_u(mark), carry);
-        const int owner = (int)owner1 - 1;
+        // the span starts are not in lane order (carried spans come first), so the scan takes the LAST mark at or
+        // before this slot, not the largest owner: (slot + 1) << 6 | owner, against the previous round's last owner
+        // (slot 0, so any mark of this round beats it)
+        const uint32_t owner1 = max(wave_inclusive_max_scan_u(mark ? (((uint32_t)lane + 1u) << 6) | (mark - 1u) : 0u),
+                                    carry);
+        const int owner = (int)(owner1 & 63u);
         const int j = base + lane;
         if (j < limit) {
             const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
@@ -1139,7 +1143,7 @@ __device__ __forceinline__ void traverse_step4c(const RenderParams& P, V3 o, V3 
             const unsigned long long kp = ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank);
             atomicMin(&L.key[owner], t >= 0.f ? kp : ~0ull);
         }
-        carry = __builtin_amdgcn_readlane(owner1, 63);
+        carry = __builtin_amdgcn_readlane(owner1, 63) & 63u;
         wave_sync();
     }
     {
