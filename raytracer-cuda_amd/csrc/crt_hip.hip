@@ -297,6 +297,7 @@ struct WaveLdsWide {
     unsigned long long key[64];
 #endif
     unsigned char owner_at[64];
+    uint32_t rays;                   // variant 8: the wave's ray count (in LDS, not a VGPR live across the loop)
 #ifdef CRT_CHECKED
     int prefix[64];                  // checked build: each owner's first pair index and pair count
     int span_n[64];
@@ -1162,6 +1163,104 @@ __device__ __forceinline__ void traverse_step4c(const RenderParams& P, V3 o, V3 
     if (COUNT) cnt.cyc_round += shader_clock() - c1;
 }
 
+// CRT_LEAF_CARRY=2: the carry without the stall.  A lane with a carried span takes its node step too, with the
+// `closest` the span was opened with (its pairs are not folded in yet): a larger bound, so its box tests may enter
+// boxes the exact bound would cull, and their primitives are tested against that bound.  The result cannot change:
+// the hit rule is the minimum (t, ~rank) over every primitive the ray's interval reaches, a superset
+// of tested primitives holds the same minimum, and `better` merges every candidate against the current closest.  Only
+// the work counters can grow.  Two spans per lane per step: the carried one (always within round 0, whose owner
+// offsets come from the owner lane's register through ds_bpermute) and the step's new one (offsets in the LDS ray
+// record).  Each step folds its per-owner minimum into (closest, hit) and clears the key.
+// One leaf round of traverse_step4d: pairs [base, base + 64) of the step's list.  FIRST (round 0) also holds the
+// carried section [0, total_c) and takes its primitive offsets from the owners' registers; later rounds never see it,
+// so the carried span's values are dead after round 0 (peeled, so they do not stay live through the round loop).
+template <bool COUNT, bool FIRST>
+__device__ __forceinline__ void leaf_round4d(const RenderParams& P, WaveLdsWide& L, int lane, int base, int limit,
+                                             int total_c, int leaf_n, int pfx, int cn, int pfx_c, int off_c,
+                                             uint32_t& carry, TraceCounts& cnt) {
+    if (COUNT) cnt.round_slots++;
+    if (FIRST && cn > 0) L.owner_at[pfx_c] = (unsigned char)(lane + 1);
+    if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)(lane + 1);
+    wave_sync();
+    const uint32_t mark = L.owner_at[lane];
+    L.owner_at[lane] = 0;
+    // span starts are not in lane order (carried spans first): the LAST mark at or before this slot
+    const uint32_t owner1 = max(wave_inclusive_max_scan_u(mark ? (((uint32_t)lane + 1u) << 6) | (mark - 1u) : 0u), carry);
+    const int owner = (int)(owner1 & 63u);
+    const int j = base + lane;
+    int oc = 0;
+    if (FIRST && total_c > 0) oc = __builtin_amdgcn_ds_bpermute(owner << 2, off_c);   // uniform branch
+    if (j < limit) {
+        const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
+        const int p = ((FIRST && j < total_c) ? oc : __float_as_int(r1.w)) + j;
+        if (COUNT) cnt.tris++;
+        int rank;
+        const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank, P.tree_spheres != 0);
+        const unsigned long long kp = ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank);
+        atomicMin(&L.key[owner], t >= 0.f ? kp : ~0ull);
+    }
+    carry = __builtin_amdgcn_readlane(owner1, 63) & 63u;
+    wave_sync();
+}
+
+// CRT_LEAF_CARRY=2: the carry without the stall.  A lane with a carried span takes its node step too, with the
+// `closest` the span was opened with (its pairs are not folded in yet): a larger bound, so its box tests may enter
+// boxes the exact bound would cull, and their primitives are tested against that bound.  The result cannot change:
+// the hit rule is the minimum (t, ~rank) over every primitive the ray's interval reaches, a superset
+// of tested primitives holds the same minimum, and `better` merges every candidate against the current closest.  Only
+// the work counters can grow.  Two spans per lane per step: the carried one (always within round 0, whose owner
+// offsets come from the owner lane's register through ds_bpermute) and the step's new one (offsets in the LDS ray
+// record).  Each step folds its per-owner minimum into (closest, hit) and clears the key.
+template <bool COUNT>
+__device__ __forceinline__ void traverse_step4d(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
+                                                float& closest, int& hit, uint32_t& pend, TraceCounts& cnt,
+                                                WaveLdsWide& L, uint32_t* __restrict__ stk, int lane, size_t pix,
+                                                size_t n_pix) {
+    if (COUNT) cnt.step_slots++;
+    const uint64_t c0 = COUNT ? shader_clock() : 0;
+    int leaf_n, leaf_first;
+    node_step4<COUNT>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
+    const uint64_t c1 = COUNT ? shader_clock() : 0;
+    if (COUNT) cnt.cyc_step += c1 - c0;
+    const int cn = (int)(pend & 0xffu);
+    if (!wave_ballot((leaf_n | cn) > 0)) return;
+    const int incl = wave_inclusive_scan_dpp((cn << 16) | leaf_n);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+    const int total_c = (int)(tot >> 16), total = total_c + (int)(tot & 0xffffu);
+    const int pfx_c = (incl >> 16) - cn;
+    const int pfx = total_c + (incl & 0xffff) - leaf_n;
+    int limit = total & ~63;
+    const int rem = total - limit;
+    if (rem != 0 && !(limit >= total_c && rem <= P.carry_max &&
+                      __popcll(wave_ballot(node >= 0)) >= P.carry_lanes))
+        limit = total;
+    L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first - pfx));
+    {
+        uint32_t ones;
+        __asm__ volatile("v_mov_b32 %0, -1" : "=v"(ones));
+        L.key[lane] = ((unsigned long long)ones << 32) | ones;
+    }
+    if (limit > 0) {
+        uint32_t carry = 0;
+        leaf_round4d<COUNT, true>(P, L, lane, 0, limit, total_c, leaf_n, pfx, cn, pfx_c, (int)(pend >> 8) - pfx_c, carry,
+                                  cnt);
+        for (int base = 64; base < limit; base += 64)
+            leaf_round4d<COUNT, false>(P, L, lane, base, limit, total_c, leaf_n, pfx, 0, 0, 0, carry, cnt);
+    }
+    {
+        const int done = min(max(limit - pfx, 0), leaf_n);
+        const unsigned long long kk = L.key[lane];
+        const float t = __uint_as_float((unsigned)(kk >> 32));
+        const int rank = (int)(0xffffffffu - (unsigned)kk);
+        if (kk != ~0ull && better(t, rank, closest, hit)) {
+            closest = t;
+            hit = rank;
+        }
+        pend = (leaf_n > done) ? (((uint32_t)(leaf_first + done) << 8) | (uint32_t)(leaf_n - done)) : 0u;
+    }
+    if (COUNT) cnt.cyc_round += shader_clock() - c1;
+}
+
 // The tree's top nodes held in LDS (CRT_TOP_LEVELS): the root and, at level 2, its internal children, copied once
 // per workgroup with their rows unswizzled (row k at 16-B slot k).  Every ray starts at the root, and its first node
 // steps are the same for every ray up to the direction signs, so a new ray takes them in the regeneration pass from
@@ -1668,6 +1767,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         V3 inv = v3(0.f, 0.f, 0.f);
         uint32_t rows = 0;         // ray_rows(inv)
         L.owner_at[lane] = 0;      // traverse_step4: owner + 1, 0 = none
+        if (TILED && lane == 0) L.rays = 0;
         constexpr bool CARRY = TILED && CRT_LEAF_CARRY != 0;
         uint32_t pend = 0;         // traverse_step4c: the lane's carried leaf span, 0 = none
         if (CARRY) L.key[lane] = ~0ull;
@@ -1723,10 +1823,13 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 live_mask = wave_ballot(has_result);
                 first_pass = false;
                 // variant 8 counts the wave's rays in a scalar (one VGPR less in the hot loop)
-                if (TILED) wave_rays += (uint32_t)__popcll(parked_mask & live_mask);
+                if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
-            if constexpr (CARRY)
+            if constexpr (CARRY && CRT_LEAF_CARRY == 2)
+                traverse_step4d<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, pend, cnt, L, stk, lane,
+                                       (size_t)pix, n_pix);
+            else if constexpr (CARRY)
                 traverse_step4c<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, pend, cnt, L, stk, lane,
                                        (size_t)pix, n_pix);
             else
@@ -1804,6 +1907,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         P.sum[3 * (size_t)pix + 1] = S.pixel.y;
         P.sum[3 * (size_t)pix + 2] = S.pixel.z;
     }
+    if constexpr (TILED) wave_rays = lds[0].rays;
     const uint64_t wr = TILED ? (uint64_t)wave_rays : wave_sum_u64(S.rays);
     if (COUNT) {
         const uint64_t wb = wave_sum_u64(cnt.boxes), wt = wave_sum_u64(cnt.tris);
