@@ -272,6 +272,10 @@ int  crt_renderer_set_top_levels(crt_renderer* r, int levels);
  * and carries a part-empty remainder of at most `max_pairs` (0..63; 0 = never) pairs to the next step when at least
  * `lanes` (0..64; 65 = never) lanes are still traversing.  Results never depend on it. */
 int  crt_renderer_set_leaf_carry(crt_renderer* r, int lanes, int max_pairs);
+/* Variant 8 with the cost probe: 1 = the blocks that share an XCD (block index mod 8, MI355X's round-robin dispatch)
+ * render one screen strip of equal probe cost, most expensive tile first, so each XCD's L2 holds its strip's geometry;
+ * 0 = one global cost order (default).  Ignored with pixel sharding.  Results never depend on it. */
+int  crt_renderer_set_xcd_regions(crt_renderer* r, int on);
 /* Pixel sharding, the bit-exact multi-GPU mode: renders of this renderer draw only shard `shard` of
  * `shards` -- the 8x8 tiles whose row-order index t has t % shards == shard, dispatched most expensive first when the
  * cost probe runs (row order without it) -- with all samples, and leave every other pixel of the linear framebuffer

@@ -309,6 +309,10 @@ class Renderer:
         check(_lib.hip().crt_renderer_last_timings(self.h, a), "last_timings")
         return {"render_ms": float(a[0]), "probe_sort_ms": float(a[1]), "main_kernel_ms": float(a[2])}
 
+    def set_xcd_regions(self, on: bool):
+        """Variant 8: XCD groups render equal-cost screen strips (crt_renderer_set_xcd_regions)."""
+        check(_lib.hip().crt_renderer_set_xcd_regions(self.h, int(bool(on))), "set_xcd_regions")
+
     def set_leaf_carry(self, lanes: int, max_pairs: int):
         """Variant 8's leaf-pair carry (CRT_LEAF_CARRY builds; crt_renderer_set_leaf_carry)."""
         check(_lib.hip().crt_renderer_set_leaf_carry(self.h, int(lanes), int(max_pairs)), "set_leaf_carry")

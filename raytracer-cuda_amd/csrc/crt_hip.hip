@@ -2265,6 +2265,87 @@ __global__ __launch_bounds__(256) void crt_order_scatter_kernel(const uint32_t* 
         if (i < n) order[h[order_bucket(cost[i])] + rank[k]] = base + (uint32_t)i;
     }
 }
+// XCD regions (crt_renderer_set_xcd_regions): MI355X deals workgroups round-robin over its 8 XCDs, so blocks b and b + 8
+// share an XCD and its 4 MiB L2 (MI355X_MICROARCH.md §Workgroup dispatch; which XCD is not fixed, and nothing depends on
+// it for correctness).  This reorders the cost-sorted tile list so that the blocks of one XCD group (b % 8 == k) render
+// one screen region: 8 vertical strips of equal probe cost (column sums of the tile keys), each in descending cost
+// (a stable partition of the sorted list).  Every group gets n/8 blocks (+1 for the first n % 8 groups): a strip with more
+// tiles than that hands its cheapest tail to a shared pool, from which the groups with fewer tiles take their last
+// blocks.  One workgroup of 1024 threads; `part` and `pool` are scratch of n entries each.  Results never depend on
+// the order (each pixel is one lane's sequential chain).
+constexpr int XCD_GROUPS = 8;
+__global__ __launch_bounds__(1024) void crt_xcd_order_kernel(uint32_t* __restrict__ order, const uint32_t* __restrict__ key,
+                                                             int n, int tiles_x, uint32_t* __restrict__ part,
+                                                             uint32_t* __restrict__ pool) {
+    __shared__ uint32_t col_region[2048];              // tiles_x <= 2048 (checked by the host)
+    __shared__ unsigned long long col_cost[2048];
+    __shared__ uint32_t wave_cnt[16][XCD_GROUPS];
+    __shared__ uint32_t reg_n[XCD_GROUPS], reg_off[XCD_GROUPS], run[XCD_GROUPS];
+    __shared__ uint32_t cap[XCD_GROUPS], exc_off[XCD_GROUPS], def_off[XCD_GROUPS];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    for (int c = t; c < tiles_x; c += 1024) col_cost[c] = 0;
+    if (t < XCD_GROUPS) run[t] = 0;
+    __syncthreads();
+    for (int i = t; i < n; i += 1024)   // a tile weighs its clamped key + 1, as the counting sort sees it
+        atomicAdd(&col_cost[i % tiles_x], (unsigned long long)(min(key[i], (uint32_t)ORDER_KEYS - 1) + 1u));
+    __syncthreads();
+    if (t == 0) {   // strips of equal cost: column c joins the strip its cost midpoint falls in
+        unsigned long long tot = 0;
+        for (int c = 0; c < tiles_x; ++c) tot += col_cost[c];
+        unsigned long long acc = 0;
+        for (int c = 0; c < tiles_x; ++c) {
+            const unsigned long long mid = acc + col_cost[c] / 2;
+            col_region[c] = (uint32_t)min((unsigned long long)XCD_GROUPS - 1, mid * XCD_GROUPS / (tot ? tot : 1));
+            acc += col_cost[c];
+        }
+    }
+    __syncthreads();
+    // stable partition of the sorted list by strip (ballot ranks inside a wave, wave totals across the workgroup)
+    for (int b0 = 0; b0 < n; b0 += 1024) {
+        const int i = b0 + t;
+        const uint32_t tile = i < n ? order[i] : 0u;
+        const uint32_t r = i < n ? col_region[tile % (uint32_t)tiles_x] : 0xffu;
+        uint32_t rank = 0;
+        for (int g = 0; g < XCD_GROUPS; ++g) {
+            const uint64_t m = __builtin_amdgcn_ballot_w64(r == (uint32_t)g);
+            if (r == (uint32_t)g) rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (lane == 0) wave_cnt[wv][g] = (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        if (r < (uint32_t)XCD_GROUPS) {
+            uint32_t before = run[r];
+            for (int w = 0; w < wv; ++w) before += wave_cnt[w][r];
+            part[(size_t)r * n + before + rank] = tile;   // strip r's list at part[r * n ...]
+        }
+        __syncthreads();
+        if (t < XCD_GROUPS)
+            for (int w = 0; w < 16; ++w) run[t] += wave_cnt[w][t];
+        __syncthreads();
+    }
+    if (t == 0) {
+        const uint32_t q = (uint32_t)n / XCD_GROUPS, e = (uint32_t)n % XCD_GROUPS;
+        uint32_t eo = 0, dd = 0;
+        for (int g = 0; g < XCD_GROUPS; ++g) {
+            reg_n[g] = run[g];
+            cap[g] = q + ((uint32_t)g < e ? 1u : 0u);
+            exc_off[g] = eo;
+            def_off[g] = dd;
+            if (run[g] > cap[g]) eo += run[g] - cap[g];
+            else dd += cap[g] - run[g];
+        }
+        (void)reg_off;
+    }
+    __syncthreads();
+    for (int g = 0; g < XCD_GROUPS; ++g)   // the strips' tails beyond their group's share, concatenated
+        for (uint32_t i = cap[g] + (uint32_t)t; i < reg_n[g]; i += 1024) pool[exc_off[g] + i - cap[g]] = part[(size_t)g * n + i];
+    __syncthreads();
+    for (int b = t; b < n; b += 1024) {
+        const int g = b % XCD_GROUPS;
+        const uint32_t i = (uint32_t)(b / XCD_GROUPS);
+        order[b] = i < reg_n[g] ? part[(size_t)g * n + i] : pool[def_off[g] + i - reg_n[g]];
+    }
+}
+
 // Variant 8: the key of an 8x8 tile is its most expensive pixel (the wave ends with its slowest lane);
 // key_mode 1 adds the mean pixel (ties between tiles with equal maxima); key_mode 2 raises a tile to 3/4 of
 // the largest key among its 8 neighbours (a 4-spp probe underestimates some tiles next to expensive ones, and an
@@ -2837,6 +2918,7 @@ struct crt_renderer {
     int crit_threshold = 16;       // (measured: profiles/r02h, r02i)
     int top_levels = -1;           // 4-wide variants: new rays' first node steps from LDS; -1 = CRT_TOP_LEVELS
     int carry_lanes = 16, carry_max = 63;   // variant 8 leaf-pair carry (builds with CRT_LEAF_CARRY)
+    int xcd_regions = 0;           // variant 8: XCD groups render screen strips (crt_xcd_order_kernel)
     int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 7 for variant 8 over >= 4 tiles per wave
                                    // slot, 6 for the other 4-wide launches and variants 3 and 10, 5 for variants 0-2
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
@@ -3456,6 +3538,10 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             hipLaunchKernelGGL(crt_order_scan_kernel, dim3(1), dim3(ORDER_KEYS), 0, st, R->d_order_hist);
             hipLaunchKernelGGL(crt_order_scatter_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key, n_tiles,
                                R->d_order_hist, R->d_order, 0u);
+            // XCD regions: the per-pixel costs are dead by now, so they hold the strips' lists and the pool (9 n_tiles)
+            if (R->xcd_regions && R->tile_shards == 1 && tiles_x <= 2048 && n_pix >= (size_t)9 * n_tiles)
+                hipLaunchKernelGGL(crt_xcd_order_kernel, dim3(1), dim3(1024), 0, st, R->d_order, R->d_tile_key, n_tiles,
+                                   tiles_x, R->d_tile_cost, R->d_tile_cost + (size_t)8 * n_tiles);
             P.order = R->d_order;
             P.crit_tiles = R->crit_tiles < 0 ? 4 * R->n_cus : R->crit_tiles;
             P.crit_threshold = R->crit_threshold;
@@ -3580,6 +3666,10 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             hipLaunchKernelGGL(crt_order_scan_kernel, dim3(1), dim3(ORDER_KEYS), 0, st, R->d_order_hist);
             hipLaunchKernelGGL(crt_order_scatter_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key, n_tiles,
                                R->d_order_hist, R->d_order, 0u);
+            // XCD regions: the per-pixel costs are dead by now, so they hold the strips' lists and the pool (9 n_tiles)
+            if (R->xcd_regions && R->tile_shards == 1 && tiles_x <= 2048 && n_pix >= (size_t)9 * n_tiles)
+                hipLaunchKernelGGL(crt_xcd_order_kernel, dim3(1), dim3(1024), 0, st, R->d_order, R->d_tile_key, n_tiles,
+                                   tiles_x, R->d_tile_cost, R->d_tile_cost + (size_t)8 * n_tiles);
             P.order = R->d_order;
         }
         const dim3 tgrid(n_tiles), tblock(64);
@@ -3798,6 +3888,12 @@ int crt_renderer_timing_history(crt_renderer* R, int back, float out[3]) {
     HIP_TRY(hipEventElapsedTime(&out[0], slot[0], slot[2]));
     HIP_TRY(hipEventElapsedTime(&out[1], slot[0], slot[1]));
     HIP_TRY(hipEventElapsedTime(&out[2], slot[1], slot[2]));
+    return CRT_OK;
+}
+
+int crt_renderer_set_xcd_regions(crt_renderer* R, int on) {
+    if (!R || on < 0 || on > 1) return set_error(CRT_ERR_INVALID_ARGUMENT, "xcd regions: 0 or 1");
+    R->xcd_regions = on;
     return CRT_OK;
 }
 

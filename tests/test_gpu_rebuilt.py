@@ -329,3 +329,21 @@ def test_shipped_instantiation_against_the_oracle(rebuilt, oracle_scenes):
     # the y0 = 950 band crosses the glass bunny (x ~1360-1600): its paths there are the frame's longest
     _, _, c = osc.render(cf, w, h, spp, 20, rect=(1360, 950, 1600, 954), nthreads=nt)
     assert c["rays"] / (240 * 4 * spp) > 1.15 * per_sample[950], (c["rays"], per_sample)
+
+
+@pytest.mark.parametrize("w,h,spp", [(640, 360, 64), (100, 37, 70), (2560, 1440, 64)])
+def test_xcd_regions_are_bit_identical(rebuilt, w, h, spp):
+    """Variant 8 with the XCD-region tile order (crt_renderer_set_xcd_regions: blocks b and b + 8 render one screen
+    strip) renders the global-order frame bit for bit: sums, RNG state and ray count; ragged sizes included."""
+    dev = rebuilt["cornell_bunny", "w4"]
+    out = []
+    for on in (0, 1):
+        r = crt_amd.Renderer(w, h)
+        r.set_xcd_regions(on)
+        r.set_camera(crt_amd.camera(spp))
+        r.init_rand(41)
+        r.render(dev, spp, 20)
+        r.synchronize()
+        assert r.last_kernel_name().startswith("crt_render_kernel<false, 8,")
+        out.append((r.linear().view(np.uint32), r.rng_state(), r.counters()["rays"]))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1]) and out[0][2] == out[1][2]
