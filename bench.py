@@ -109,6 +109,8 @@ def parse():
                     help="variant 8 leaf-pair carry (crt_renderer_set_leaf_carry; CRT_LEAF_CARRY builds)")
     ap.add_argument("--xcd-regions", type=int, default=None, choices=[0, 1],
                     help="variant 8: XCD groups render equal-cost screen strips (crt_renderer_set_xcd_regions)")
+    ap.add_argument("--rejection-cap", type=int, default=None,
+                    help="variant 8: unit-sphere candidates per pass before a lane waits (crt_renderer_set_rejection_cap)")
     ap.add_argument("--bvh", default="rebuilt", choices=["rebuilt", "reference"])
     ap.add_argument("--bvh-width", type=int, default=4, help="rebuilt BVH: 4 (variant 4) or 2 (threaded)")
     ap.add_argument("--leaf-size", type=int, default=4)
@@ -371,6 +373,8 @@ def main():
         r.set_leaf_carry(*args.carry)
     if args.xcd_regions is not None:
         r.set_xcd_regions(args.xcd_regions)
+    if args.rejection_cap is not None:
+        r.set_rejection_cap(args.rejection_cap)
     r.set_camera(cam)
     fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard,
                               collective=grouped)

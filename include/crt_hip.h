@@ -272,6 +272,10 @@ int  crt_renderer_set_top_levels(crt_renderer* r, int levels);
  * and carries a part-empty remainder of at most `max_pairs` (0..63; 0 = never) pairs to the next step when at least
  * `lanes` (0..64; 65 = never) lanes are still traversing.  Results never depend on it. */
 int  crt_renderer_set_leaf_carry(crt_renderer* r, int lanes, int max_pairs);
+/* Variant 8: a regeneration pass draws at most `candidates` unit-sphere candidates (Lambertian and Metal scatter's
+ * rejection loop, Utility.cuh:45-53) per lane; a lane that rejected them all keeps its hit and stays parked, and the next
+ * pass continues its draws.  0 = no cap (default).  The critical tiles never defer.  Results never depend on it. */
+int  crt_renderer_set_rejection_cap(crt_renderer* r, int candidates);
 /* Variant 8 with the cost probe: 1 = the blocks that share an XCD (block index mod 8, MI355X's round-robin dispatch)
  * render one screen strip of equal probe cost, most expensive tile first, so each XCD's L2 holds its strip's geometry;
  * 0 = one global cost order (default).  Ignored with pixel sharding.  Results never depend on it. */

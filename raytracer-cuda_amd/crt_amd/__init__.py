@@ -309,6 +309,10 @@ class Renderer:
         check(_lib.hip().crt_renderer_last_timings(self.h, a), "last_timings")
         return {"render_ms": float(a[0]), "probe_sort_ms": float(a[1]), "main_kernel_ms": float(a[2])}
 
+    def set_rejection_cap(self, candidates: int):
+        """Variant 8: unit-sphere candidates per pass before a lane waits for the next pass (crt_renderer_set_rejection_cap)."""
+        check(_lib.hip().crt_renderer_set_rejection_cap(self.h, int(candidates)), "set_rejection_cap")
+
     def set_xcd_regions(self, on: bool):
         """Variant 8: XCD groups render equal-cost screen strips (crt_renderer_set_xcd_regions)."""
         check(_lib.hip().crt_renderer_set_xcd_regions(self.h, int(bool(on))), "set_xcd_regions")

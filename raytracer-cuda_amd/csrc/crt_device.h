@@ -151,6 +151,27 @@ __device__ __forceinline__ float uniform(Rng& s) { return __builtin_fmaf((float)
 // multiply fewer than the literal restatement, the same bits.
 __device__ __forceinline__ float rand_pm1(Rng& s) { return __builtin_fmaf(uniform(s), 2.0f, -1.0f); }
 
+// rand_unit_vector with at most `cap` candidates (0 = no cap): `done` is false when the lane rejected all of them.  The
+// rejected candidates only advanced the lane's RNG state, so calling it again later continues the reference's loop
+// exactly where it stopped.
+__device__ __forceinline__ V3 rand_unit_vector_capped(Rng& s, int cap, bool& done) {
+    V3 p;
+    int it = 0;
+    for (;;) {
+        float a = rand_pm1(s);
+        float b = rand_pm1(s);
+        float c = rand_pm1(s);
+        p = v3(a, b, c);
+        if (!(len2(p) >= 1)) {
+            done = true;
+            return unit(p);
+        }
+        if (++it == cap) {
+            done = false;
+            return p;
+        }
+    }
+}
 __device__ __forceinline__ V3 rand_unit_vector(Rng& s) {   // Utility.cuh:45-53, :73-76
     V3 p;
     for (;;) {

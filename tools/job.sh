@@ -1,13 +1,13 @@
 #!/bin/bash
 # The current one-off GPU job (overwritten per job; the copy that ran is kept as profiles/<id>/job.sh).
 # r04d: XCD-region tile order (crt_renderer_set_xcd_regions): bit-identity test, A/B on configs C and E, L2 hit rate
-# with and without; then a first PC-sampling trial (rocprofv3 host_trap, short frame) as the last step.
+# with and without; the unit-sphere rejection cap (crt_renderer_set_rejection_cap): bits and an A/B against HEAD's build.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=r04d; OUT=$R/gpurun_out/$O; mkdir -p $OUT
 cd $R
 sha256sum raytracer-cuda_amd/csrc/crt_hip.hip raytracer-cuda_amd/lib/libcrt_hip.so > $OUT/sha.txt
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_rebuilt.py -m gpu -x -q -k xcd --timeout 200 --timeout-method thread > $OUT/pytest_xcd.log 2>&1
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_rebuilt.py -m gpu -x -q -k 'xcd or rejection_cap' --timeout 200 --timeout-method thread > $OUT/pytest_xcd.log 2>&1
 tail -1 $OUT/pytest_xcd.log
 timeout -k 10 200 python3 tools/frame_hash.py --big > $OUT/hash_off.txt 2>&1
 timeout -k 10 200 python3 tools/frame_hash.py --big --xcd-regions 1 > $OUT/hash_on.txt 2>&1
@@ -19,6 +19,14 @@ for i in 1 2 3; do
   timeout -k 10 300 $B --scene cornell_1m --spp 512 --xcd-regions 0 > $OUT/E_off_$i.log 2>&1
   timeout -k 10 300 $B --scene cornell_1m --spp 512 --xcd-regions 1 > $OUT/E_on_$i.log 2>&1
   for f in C_off C_on E_off E_on; do echo "$f round $i: $(grep -o '"main_kernel_ms": [0-9.]*' $OUT/${f}_$i.log | tail -1)"; done
+done
+BASE=$R/raytracer-cuda_amd/lib_exp/base/libcrt_hip.so
+timeout -k 10 200 python3 tools/frame_hash.py --big --rejection-cap 3 > $OUT/hash_cap3.txt 2>&1
+cmp $OUT/hash_off.txt $OUT/hash_cap3.txt && echo "cap3: hashes identical" || echo "cap3: HASHES DIFFER"
+for i in 1 2 3; do
+  CRT_HIP_LIB=$BASE timeout -k 10 300 $B > $OUT/base_$i.log 2>&1
+  for c in 0 3 4 6; do timeout -k 10 300 $B --rejection-cap $c > $OUT/cap${c}_$i.log 2>&1; done
+  for f in base cap0 cap3 cap4 cap6; do echo "$f round $i: $(grep -o '"main_kernel_ms": [0-9.]*' $OUT/${f}_$i.log | tail -1)"; done
 done
 cd /tmp && export TMPDIR=/tmp
 for x in 0 1; do
