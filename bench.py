@@ -102,6 +102,8 @@ def parse():
     ap.add_argument("--probe-spp", type=int, default=None,
                     help="cost-probe samples per pixel before a variant-8 render (default: the library's automatic "
                          "choice, 4 for >= 1000 spp else 2; 0 = no probe)")
+    ap.add_argument("--probe-stride", type=int, default=1, choices=[1, 2, 4],
+                    help="variant 8's cost probe on every 1st / 2nd / 4th pixel in x and y (crt_renderer_set_schedule)")
     ap.add_argument("--critical-tiles", type=int, default=None,
                     help="variant 8: leading tiles of the cost order that regenerate sooner (default: library's)")
     ap.add_argument("--critical-lanes", type=int, default=16, help="their regeneration threshold")
@@ -365,8 +367,8 @@ def main():
         r.set_regen_threshold(args.regen_threshold)
     if args.occupancy is not None:
         r.set_occupancy_target(args.occupancy)
-    if args.probe_spp is not None:
-        r.set_schedule(args.probe_spp, 64)
+    if args.probe_spp is not None or args.probe_stride != 1:
+        r.set_schedule(-1 if args.probe_spp is None else args.probe_spp, 64, probe_stride=args.probe_stride)
     if args.critical_tiles is not None:
         r.set_critical_tiles(args.critical_tiles, args.critical_lanes)
     if args.carry is not None:

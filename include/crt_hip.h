@@ -250,7 +250,8 @@ int  crt_renderer_set_kernel_variant(crt_renderer* r, int variant);
  * most-expensive-first (variant 7: pixels handed to lanes from a global queue; variant 8: 8x8 tiles, one wave per
  * workgroup).  Renders with fewer than min_spp samples per pixel skip the probe.  flags bits 16-19: variant 8's tile
  * key (0 = slowest pixel, 1 = slowest + mean pixel, 2 = 0 raised to 3/4 of the neighbours'; the renderer starts with
- * 2, the measured best); other bits are ignored.
+ * 2, the measured best); bits 20-23: variant 8's probe stride (0 or 1 = every pixel, 2 or 4 = every 2nd / 4th pixel in
+ * x and y, 1/4 or 1/16 of the probe's work); other bits are ignored.
  * Default -1 (automatic: 4 probe samples for renders of >= 1000 spp, else 2), 64, 2 << 16; probe_spp 0 disables the
  * probe.  Results never depend on the order. */
 int  crt_renderer_set_schedule(crt_renderer* r, int probe_spp, int min_spp, int flags);

@@ -220,8 +220,8 @@ class Renderer:
     def init_rand(self, seed: int = 41, subsequence_base: int = 0, stream=None):
         check(_lib.hip().crt_renderer_init_rand(self.h, int(seed), int(subsequence_base), stream), "init_rand")
 
-    def set_schedule(self, probe_spp: int = -1, min_spp: int = 64, tile_key: int = 2):
-        flags = (int(tile_key) & 0xf) << 16
+    def set_schedule(self, probe_spp: int = -1, min_spp: int = 64, tile_key: int = 2, probe_stride: int = 1):
+        flags = ((int(tile_key) & 0xf) << 16) | ((int(probe_stride) & 0xf) << 20)
         check(_lib.hip().crt_renderer_set_schedule(self.h, int(probe_spp), int(min_spp), flags), "set_schedule")
 
     def set_critical_tiles(self, tiles: int = -1, lanes: int = 16):

@@ -76,6 +76,7 @@ struct RenderParams {
     int n_slots;
     int tiles_x;                          // variant 8: 8x8 tiles per row (order[] holds tile indices)
     uint32_t* __restrict__ probe_cost;    // probe launch (variant 4): rays per pixel; nothing else is written
+    int probe_stride;                     // probe launch (variant 4): lanes take every probe_stride-th pixel in x and y
     int crit_tiles, crit_threshold;       // variant 8: the first crit_tiles tiles of the cost order regenerate at
                                           // crit_threshold parked lanes instead of regen_threshold
     int top_levels;                       // 4-wide variants: a new ray's first node steps taken from LDS (<= CRT_TOP_LEVELS)
@@ -1467,11 +1468,15 @@ __device__ __forceinline__ void shade_rec(PathState& S, const RenderParams& P, i
         // with a cap (variant 8, CRT tuning `reject_cap`), a lane whose candidates all missed the unit sphere stops
         // here and changes nothing but its RNG state; it stays parked with the same hit, and the next pass re-runs
         // finish_ray, which continues its draws
-        bool done = true;
-        ruv = rand_unit_vector_capped(S.s, reject_cap, done);
-        if (!done) {
-            *deferred = true;
-            return;
+        if (reject_cap == 0) {   // wave-uniform: the reference's loop as it is
+            ruv = rand_unit_vector(S.s);
+        } else {
+            bool done;
+            ruv = rand_unit_vector_capped(S.s, reject_cap, done);
+            if (!done) {
+                *deferred = true;
+                return;
+            }
         }
     }
     if (code == SHADE_LAMBERT) {                         // Material.cuh:66-77
@@ -1625,6 +1630,10 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     } else {
         x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
         y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+        if (VARIANT == 4 && P.probe_cost) {   // a subsampled cost probe (crt_renderer_set_schedule's stride)
+            x *= P.probe_stride;
+            y *= P.probe_stride;
+        }
     }
     const bool valid = x < P.width && y < P.height;
     const int pix = valid ? y * P.width + x : 0;
@@ -1788,8 +1797,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
         const int regen_t = (TILED && (int)blockIdx.x < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
         // variant 8: candidates of the unit-sphere rejection loop per pass before a lane is deferred to the next pass
-        // (0 = no cap; never for the critical tiles, whose sample chains bound short frames)
-        const int reject_cap = (TILED && (int)blockIdx.x >= P.crit_tiles) ? P.reject_cap : 0;
+        // (0 = no cap)
+        const int reject_cap = TILED ? P.reject_cap : 0;
         bool first_pass = true;    // uniform
         for (;;) {
             // a lane whose trace ended but whose carried leaf pairs are untested is not parked yet
@@ -2372,13 +2381,13 @@ __global__ __launch_bounds__(1024) void crt_xcd_order_kernel(uint32_t* __restric
 // the largest key among its 8 neighbours (a 4-spp probe underestimates some tiles next to expensive ones, and an
 // underestimated tile dispatched late becomes the launch's tail).
 __global__ void crt_tile_cost_kernel(const uint32_t* __restrict__ pix_cost, int width, int height, int tiles_x,
-                                     int n_tiles, uint32_t* __restrict__ tile_cost, int key_mode) {
+                                     int n_tiles, uint32_t* __restrict__ tile_cost, int key_mode, int stride) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tiles) return;
     const int x0 = (t % tiles_x) * 8, y0 = (t / tiles_x) * 8;
     uint32_t m = 0, sum = 0, k = 0;
-    for (int y = y0; y < min(height, y0 + 8); ++y)
-        for (int x = x0; x < min(width, x0 + 8); ++x) {
+    for (int y = y0; y < min(height, y0 + 8); y += stride)   // a subsampled probe wrote pixels with x, y % stride == 0
+        for (int x = x0; x < min(width, x0 + 8); x += stride) {
             const uint32_t c = pix_cost[(size_t)y * width + x];
             m = max(m, c);
             sum += c;
@@ -2940,6 +2949,7 @@ struct crt_renderer {
     int top_levels = -1;           // 4-wide variants: new rays' first node steps from LDS; -1 = CRT_TOP_LEVELS
     int carry_lanes = 16, carry_max = 63;   // variant 8 leaf-pair carry (builds with CRT_LEAF_CARRY)
     int xcd_regions = 0;           // variant 8: XCD groups render screen strips (crt_xcd_order_kernel)
+    int probe_stride = 1;          // variant 8's cost probe: every probe_stride-th pixel in x and y
     int reject_cap = 0;            // variant 8: unit-sphere candidates per pass before a lane waits for the next pass
     int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 7 for variant 8 over >= 4 tiles per wave
                                    // slot, 6 for the other 4-wide launches and variants 3 and 10, 5 for variants 0-2
@@ -3363,6 +3373,10 @@ int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int f
     R->probe_spp = probe_spp < 0 ? -1 : probe_spp;
     R->probe_min_spp = min_spp;
     R->tile_key_mode = (flags >> 16) & 0xf;   // 0 = slowest pixel (callers that pass 0 get the plain key)
+    const int stride = (flags >> 20) & 0xf;   // variant 8's probe subsampling: 0 = 1 (every pixel), 2, 4
+    if (stride != 0 && stride != 1 && stride != 2 && stride != 4)
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "probe stride (flags >> 20): 1, 2 or 4");
+    R->probe_stride = stride ? stride : 1;
     return CRT_OK;
 }
 
@@ -3442,6 +3456,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.accumulate = (flags & CRT_RENDER_ACCUMULATE) ? 1 : 0;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     P.rcp_w = R->rcp_w; P.rcp_h = R->rcp_h; P.fast_uv = R->fast_uv;
+    P.probe_stride = 1;
     P.ovf = nullptr;
     P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0; P.crit_tiles = 0; P.crit_threshold = 64;
     P.top_levels = R->top_levels < 0 ? CRT_TOP_LEVELS : R->top_levels;
@@ -3543,10 +3558,13 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             Q.spp = probe_spp_for(R, spp);
             Q.accumulate = 0;
             Q.probe_cost = R->d_tile_cost;
-            if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<true, 4, 6>), grid, block, 0, st, Q);
-            else hipLaunchKernelGGL((crt_render_kernel<true, 4, 5>), grid, block, 0, st, Q);
+            Q.probe_stride = R->probe_stride;   // 1, 2 or 4: every stride-th pixel in x and y
+            const int ps = 16 * R->probe_stride;
+            const dim3 pgrid((R->width + ps - 1) / ps, (R->height + ps - 1) / ps);
+            if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<true, 4, 6>), pgrid, block, 0, st, Q);
+            else hipLaunchKernelGGL((crt_render_kernel<true, 4, 5>), pgrid, block, 0, st, Q);
             hipLaunchKernelGGL(crt_tile_cost_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_tile_cost,
-                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode);
+                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode, R->probe_stride);
             if (R->tile_key_mode == 2) {   // per-pixel costs are no longer needed: reuse them for the smoothed keys
                 hipLaunchKernelGGL(crt_tile_neighbour_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st,
                                    R->d_tile_key, tiles_x, n_tiles, R->d_tile_cost);
@@ -3677,7 +3695,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             Q.probe_cost = R->d_tile_cost;
             hipLaunchKernelGGL((crt_render_kernel<true, 3, 5>), grid, block, 0, st, Q);
             hipLaunchKernelGGL(crt_tile_cost_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_tile_cost,
-                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode);
+                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode, 1);
             if (R->tile_key_mode == 2) {
                 hipLaunchKernelGGL(crt_tile_neighbour_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st,
                                    R->d_tile_key, tiles_x, n_tiles, R->d_tile_cost);
@@ -3755,6 +3773,7 @@ int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene*
     P.accumulate = 0; P.regen_threshold = 64;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     P.rcp_w = R->rcp_w; P.rcp_h = R->rcp_h; P.fast_uv = R->fast_uv;
+    P.probe_stride = 1;
     Q.nodes_b = B->d_nodes; Q.prims_b = B->d_prims; Q.n_nodes_b = B->n_nodes; Q.n_layouts_b = B->layouts;
     Q.width_a = A->width; Q.width_b = B->width;
     Q.dump = nullptr;

@@ -368,3 +368,22 @@ def test_rejection_cap_is_bit_identical(rebuilt, cap):
         assert r.last_kernel_name() == "crt_render_kernel<false, 8, 7>"
         out.append((r.linear().view(np.uint32), r.rng_state(), r.counters()["rays"]))
     assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1]) and out[0][2] == out[1][2]
+
+
+@pytest.mark.parametrize("stride", [2, 4])
+def test_probe_stride_is_bit_identical(rebuilt, stride):
+    """Variant 8 with a subsampled cost probe (every 2nd / 4th pixel in x and y): only the tile order changes, so the
+    frame, RNG state and ray count equal the full probe's; a ragged size checks the edge tiles."""
+    dev = rebuilt["cornell_bunny", "w4"]
+    for w, h, spp in ((2560, 1440, 64), (100, 37, 70)):
+        out = []
+        for s in (1, stride):
+            r = crt_amd.Renderer(w, h)
+            r.set_schedule(-1, 64, probe_stride=s)
+            r.set_camera(crt_amd.camera(spp))
+            r.init_rand(41)
+            r.render(dev, spp, 20)
+            r.synchronize()
+            assert r.last_timings()["probe_sort_ms"] > 0
+            out.append((r.linear().view(np.uint32), r.rng_state(), r.counters()["rays"]))
+        assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1]) and out[0][2] == out[1][2]
