@@ -102,8 +102,9 @@ def parse():
     ap.add_argument("--probe-spp", type=int, default=None,
                     help="cost-probe samples per pixel before a variant-8 render (default: the library's automatic "
                          "choice, 4 for >= 1000 spp else 2; 0 = no probe)")
-    ap.add_argument("--probe-stride", type=int, default=1, choices=[1, 2, 4],
-                    help="variant 8's cost probe on every 1st / 2nd / 4th pixel in x and y (crt_renderer_set_schedule)")
+    ap.add_argument("--probe-stride", type=int, default=0, choices=[0, 1, 2, 4],
+                    help="variant 8's cost probe on every 1st / 2nd / 4th pixel in x and y (crt_renderer_set_schedule; "
+                         "0 = the library's automatic choice: 2 below 1000 spp, else 1)")
     ap.add_argument("--critical-tiles", type=int, default=None,
                     help="variant 8: leading tiles of the cost order that regenerate sooner (default: library's)")
     ap.add_argument("--critical-lanes", type=int, default=16, help="their regeneration threshold")
@@ -111,8 +112,6 @@ def parse():
                     help="variant 8 leaf-pair carry (crt_renderer_set_leaf_carry; CRT_LEAF_CARRY builds)")
     ap.add_argument("--xcd-regions", type=int, default=None, choices=[0, 1],
                     help="variant 8: XCD groups render equal-cost screen strips (crt_renderer_set_xcd_regions)")
-    ap.add_argument("--rejection-cap", type=int, default=None,
-                    help="variant 8: unit-sphere candidates per pass before a lane waits (crt_renderer_set_rejection_cap)")
     ap.add_argument("--bvh", default="rebuilt", choices=["rebuilt", "reference"])
     ap.add_argument("--bvh-width", type=int, default=4, help="rebuilt BVH: 4 (variant 4) or 2 (threaded)")
     ap.add_argument("--leaf-size", type=int, default=4)
@@ -367,7 +366,7 @@ def main():
         r.set_regen_threshold(args.regen_threshold)
     if args.occupancy is not None:
         r.set_occupancy_target(args.occupancy)
-    if args.probe_spp is not None or args.probe_stride != 1:
+    if args.probe_spp is not None or args.probe_stride:
         r.set_schedule(-1 if args.probe_spp is None else args.probe_spp, 64, probe_stride=args.probe_stride)
     if args.critical_tiles is not None:
         r.set_critical_tiles(args.critical_tiles, args.critical_lanes)
@@ -375,8 +374,6 @@ def main():
         r.set_leaf_carry(*args.carry)
     if args.xcd_regions is not None:
         r.set_xcd_regions(args.xcd_regions)
-    if args.rejection_cap is not None:
-        r.set_rejection_cap(args.rejection_cap)
     r.set_camera(cam)
     fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard,
                               collective=grouped)

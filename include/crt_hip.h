@@ -250,8 +250,8 @@ int  crt_renderer_set_kernel_variant(crt_renderer* r, int variant);
  * most-expensive-first (variant 7: pixels handed to lanes from a global queue; variant 8: 8x8 tiles, one wave per
  * workgroup).  Renders with fewer than min_spp samples per pixel skip the probe.  flags bits 16-19: variant 8's tile
  * key (0 = slowest pixel, 1 = slowest + mean pixel, 2 = 0 raised to 3/4 of the neighbours'; the renderer starts with
- * 2, the measured best); bits 20-23: variant 8's probe stride (0 or 1 = every pixel, 2 or 4 = every 2nd / 4th pixel in
- * x and y, 1/4 or 1/16 of the probe's work); other bits are ignored.
+ * 2, the measured best); bits 20-23: variant 8's probe stride (1 = every pixel, 2 or 4 = every 2nd / 4th pixel in x and
+ * y, 1/4 or 1/16 of the probe's work; 0 = automatic: 2 below 1000 spp, else 1); other bits are ignored.
  * Default -1 (automatic: 4 probe samples for renders of >= 1000 spp, else 2), 64, 2 << 16; probe_spp 0 disables the
  * probe.  Results never depend on the order. */
 int  crt_renderer_set_schedule(crt_renderer* r, int probe_spp, int min_spp, int flags);
@@ -273,10 +273,6 @@ int  crt_renderer_set_top_levels(crt_renderer* r, int levels);
  * and carries a part-empty remainder of at most `max_pairs` (0..63; 0 = never) pairs to the next step when at least
  * `lanes` (0..64; 65 = never) lanes are still traversing.  Results never depend on it. */
 int  crt_renderer_set_leaf_carry(crt_renderer* r, int lanes, int max_pairs);
-/* Variant 8: a regeneration pass draws at most `candidates` unit-sphere candidates (Lambertian and Metal scatter's
- * rejection loop, Utility.cuh:45-53) per lane; a lane that rejected them all keeps its hit and stays parked, and the next
- * pass continues its draws.  0 = no cap (default).  The critical tiles never defer.  Results never depend on it. */
-int  crt_renderer_set_rejection_cap(crt_renderer* r, int candidates);
 /* Variant 8 with the cost probe: 1 = the blocks that share an XCD (block index mod 8, MI355X's round-robin dispatch)
  * render one screen strip of equal probe cost, most expensive tile first, so each XCD's L2 holds its strip's geometry;
  * 0 = one global cost order (default).  Ignored with pixel sharding.  Results never depend on it. */

@@ -220,7 +220,7 @@ class Renderer:
     def init_rand(self, seed: int = 41, subsequence_base: int = 0, stream=None):
         check(_lib.hip().crt_renderer_init_rand(self.h, int(seed), int(subsequence_base), stream), "init_rand")
 
-    def set_schedule(self, probe_spp: int = -1, min_spp: int = 64, tile_key: int = 2, probe_stride: int = 1):
+    def set_schedule(self, probe_spp: int = -1, min_spp: int = 64, tile_key: int = 2, probe_stride: int = 0):
         flags = ((int(tile_key) & 0xf) << 16) | ((int(probe_stride) & 0xf) << 20)
         check(_lib.hip().crt_renderer_set_schedule(self.h, int(probe_spp), int(min_spp), flags), "set_schedule")
 
@@ -308,10 +308,6 @@ class Renderer:
         a = (C.c_float * 3)()
         check(_lib.hip().crt_renderer_last_timings(self.h, a), "last_timings")
         return {"render_ms": float(a[0]), "probe_sort_ms": float(a[1]), "main_kernel_ms": float(a[2])}
-
-    def set_rejection_cap(self, candidates: int):
-        """Variant 8: unit-sphere candidates per pass before a lane waits for the next pass (crt_renderer_set_rejection_cap)."""
-        check(_lib.hip().crt_renderer_set_rejection_cap(self.h, int(candidates)), "set_rejection_cap")
 
     def set_xcd_regions(self, on: bool):
         """Variant 8: XCD groups render equal-cost screen strips (crt_renderer_set_xcd_regions)."""

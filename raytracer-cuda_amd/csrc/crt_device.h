@@ -151,26 +151,6 @@ __device__ __forceinline__ float uniform(Rng& s) { return __builtin_fmaf((float)
 // multiply fewer than the literal restatement, the same bits.
 __device__ __forceinline__ float rand_pm1(Rng& s) { return __builtin_fmaf(uniform(s), 2.0f, -1.0f); }
 
-// rand_unit_vector with at most `cap` (>= 1) candidates per lane: `done` is false when the lane rejected all of them.  The
-// rejected candidates only advanced the lane's RNG state, so calling it again later continues the reference's loop
-// exactly where it stopped.  The loop is wave-uniform (a lane that accepted skips the body), so the cap is one scalar
-// compare per iteration.
-__device__ __forceinline__ V3 rand_unit_vector_capped(Rng& s, int cap, bool& done) {
-    V3 p = v3(0.f, 0.f, 0.f);
-    bool pending = true;
-    for (int it = 1;; ++it) {
-        if (pending) {
-            float a = rand_pm1(s);
-            float b = rand_pm1(s);
-            float c = rand_pm1(s);
-            p = v3(a, b, c);
-            pending = len2(p) >= 1;
-        }
-        if (!__builtin_amdgcn_ballot_w64(pending) || it == cap) break;
-    }
-    done = !pending;
-    return done ? unit(p) : p;
-}
 __device__ __forceinline__ V3 rand_unit_vector(Rng& s) {   // Utility.cuh:45-53, :73-76
     V3 p;
     for (;;) {

@@ -80,7 +80,6 @@ struct RenderParams {
     int crit_tiles, crit_threshold;       // variant 8: the first crit_tiles tiles of the cost order regenerate at
                                           // crit_threshold parked lanes instead of regen_threshold
     int top_levels;                       // 4-wide variants: a new ray's first node steps taken from LDS (<= CRT_TOP_LEVELS)
-    int reject_cap;                       // variant 8: unit-sphere candidates per pass before a lane waits (0 = none)
     int carry_lanes, carry_max;           // variant 8 leaf-pair carry (traverse_step4c): a step's part-empty round of
                                           // at most carry_max pairs waits for the next step when at least carry_lanes
                                           // lanes are still traversing
@@ -1428,8 +1427,7 @@ __device__ __forceinline__ bool cannot_refract_exact(float cos_theta, float ri) 
 // shade_rec: the same with the hit's shading record rows 0-1 already loaded (r0, m); a sphere's row 2 (1 / radius) is
 // inv_r when `staged`, else loaded here.
 __device__ __forceinline__ void shade_rec(PathState& S, const RenderParams& P, int hit_rank, float t, float4 r0,
-                                          float4 m, bool staged, float inv_r, int reject_cap = 0,
-                                          bool* deferred = nullptr);
+                                          float4 m, bool staged, float inv_r);
 __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int hit_rank, float t) {
     float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), m = r0;
     if (hit_rank >= 0) {
@@ -1440,7 +1438,7 @@ __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int h
     shade_rec(S, P, hit_rank, t, r0, m, false, 0.f);
 }
 __device__ __forceinline__ void shade_rec(PathState& S, const RenderParams& P, int hit_rank, float t, float4 r0,
-                                          float4 m, bool staged, float inv_r, int reject_cap, bool* deferred) {
+                                          float4 m, bool staged, float inv_r) {
     if (hit_rank < 0) {                                  // :137-142
         S.pixel = S.pixel + S.thr * sky(S.d);
         ++S.paths;
@@ -1464,21 +1462,7 @@ __device__ __forceinline__ void shade_rec(PathState& S, const RenderParams& P, i
     // Lambertian and Metal both draw one randomUnitVector first (their only draws): one rejection loop for
     // both, so a wave holding both materials does not run the loop twice.
     V3 ruv;
-    if (code == SHADE_LAMBERT || code == SHADE_METAL) {
-        // with a cap (variant 8, CRT tuning `reject_cap`), a lane whose candidates all missed the unit sphere stops
-        // here and changes nothing but its RNG state; it stays parked with the same hit, and the next pass re-runs
-        // finish_ray, which continues its draws
-        if (reject_cap == 0) {   // wave-uniform: the reference's loop as it is
-            ruv = rand_unit_vector(S.s);
-        } else {
-            bool done;
-            ruv = rand_unit_vector_capped(S.s, reject_cap, done);
-            if (!done) {
-                *deferred = true;
-                return;
-            }
-        }
-    }
+    if (code == SHADE_LAMBERT || code == SHADE_METAL) ruv = rand_unit_vector(S.s);
     if (code == SHADE_LAMBERT) {                         // Material.cuh:66-77
         V3 sd = n + ruv;
         if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = n;
@@ -1527,8 +1511,7 @@ __device__ __forceinline__ void shade_rec(PathState& S, const RenderParams& P, i
 // wins, its record comes from the LDS copy of the two per-ray spheres' records (or from HBM for other sphere counts).
 template <bool COUNT>
 __device__ __forceinline__ void finish_ray(PathState& S, const RenderParams& P, V3 inv, float closest, int hit,
-                                           const float* sph_lds, const float4* shd_lds, TraceCounts& cnt, uint64_t s0,
-                                           int reject_cap = 0, bool* deferred = nullptr) {
+                                           const float* sph_lds, const float4* shd_lds, TraceCounts& cnt, uint64_t s0) {
     const int h0 = hit;
     float4 e0 = make_float4(0.f, 0.f, 0.f, 0.f), e1 = e0;
     if (h0 >= 0) {
@@ -1555,7 +1538,7 @@ __device__ __forceinline__ void finish_ray(PathState& S, const RenderParams& P, 
             e1 = Rh[1];
         }
     }
-    shade_rec(S, P, hit, closest, e0, e1, staged, inv_r, reject_cap, deferred);
+    shade_rec(S, P, hit, closest, e0, e1, staged, inv_r);
 }
 
 // VARIANT 0: per-lane traversal (leaf loops inside the lane).  VARIANT 1: cooperative leaves.
@@ -1796,9 +1779,6 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         // variant 8: the most expensive tiles of the cost order bound the frame when it has few tiles per wave slot
         // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
         const int regen_t = (TILED && (int)blockIdx.x < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
-        // variant 8: candidates of the unit-sphere rejection loop per pass before a lane is deferred to the next pass
-        // (0 = no cap)
-        const int reject_cap = TILED ? P.reject_cap : 0;
         bool first_pass = true;    // uniform
         for (;;) {
             // a lane whose trace ended but whose carried leaf pairs are untested is not parked yet
@@ -1809,7 +1789,6 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             const uint64_t c0 = COUNT ? shader_clock() : 0;
             if (n_parked >= regen_t || n_parked == n_live) {
                 if (COUNT) cnt.passes++;
-                bool deferred = false;
                 if (__builtin_amdgcn_inverse_ballot_w64(parked_mask)) {
                     const uint64_t s0 = COUNT ? shader_clock() : 0;
                     // (loading the shading record before this sphere test, to overlap its latency, measured +0.7 %:
@@ -1818,18 +1797,17 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     // the lanes with a ray): a uniform test instead of a divergent branch on has_result (-0.38 %,
                     // profiles/r02av)
                     if (!first_pass) {
-                        finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, s0, reject_cap, &deferred);
+                        finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, s0);
                     }
                     const uint64_t s1 = COUNT ? shader_clock() : 0;
-                    // a deferred lane (its unit-sphere draws hit the cap) keeps its hit and stays parked: no next ray
-                    const bool live = deferred || next_ray(S, C, x, y, P.max_bounces);
+                    const bool live = next_ray(S, C, x, y, P.max_bounces);
                     if (COUNT) {
                         const uint64_t s2 = shader_clock();
                         cnt.cyc_shade += s1 - s0;
                         cnt.cyc_next += s2 - s1;
                     }
-                    has_result = deferred;
-                    if (live && !deferred) {
+                    has_result = false;
+                    if (live) {
                         if (!TILED) ++S.rays;
                         has_result = true;
                         node = 0;
@@ -1849,11 +1827,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 }
                 live_mask = wave_ballot(has_result);
                 first_pass = false;
-                // variant 8 counts the wave's rays in LDS (one VGPR less in the hot loop); deferred lanes start none
-                if (TILED) {
-                    const uint64_t started = parked_mask & live_mask & ~wave_ballot(deferred);
-                    if (lane == 0) L.rays += (uint32_t)__popcll(started);
-                }
+                // variant 8 counts the wave's rays in LDS (one VGPR less in the hot loop)
+                if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
             if constexpr (CARRY && CRT_LEAF_CARRY == 2)
@@ -2949,8 +2924,7 @@ struct crt_renderer {
     int top_levels = -1;           // 4-wide variants: new rays' first node steps from LDS; -1 = CRT_TOP_LEVELS
     int carry_lanes = 16, carry_max = 63;   // variant 8 leaf-pair carry (builds with CRT_LEAF_CARRY)
     int xcd_regions = 0;           // variant 8: XCD groups render screen strips (crt_xcd_order_kernel)
-    int probe_stride = 1;          // variant 8's cost probe: every probe_stride-th pixel in x and y
-    int reject_cap = 0;            // variant 8: unit-sphere candidates per pass before a lane waits for the next pass
+    int probe_stride = 0;          // variant 8's cost probe: every probe_stride-th pixel in x and y (0 = automatic)
     int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 7 for variant 8 over >= 4 tiles per wave
                                    // slot, 6 for the other 4-wide launches and variants 3 and 10, 5 for variants 0-2
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
@@ -3373,10 +3347,10 @@ int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int f
     R->probe_spp = probe_spp < 0 ? -1 : probe_spp;
     R->probe_min_spp = min_spp;
     R->tile_key_mode = (flags >> 16) & 0xf;   // 0 = slowest pixel (callers that pass 0 get the plain key)
-    const int stride = (flags >> 20) & 0xf;   // variant 8's probe subsampling: 0 = 1 (every pixel), 2, 4
+    const int stride = (flags >> 20) & 0xf;   // variant 8's probe subsampling: 0 = automatic, 1 (every pixel), 2, 4
     if (stride != 0 && stride != 1 && stride != 2 && stride != 4)
-        return set_error(CRT_ERR_INVALID_ARGUMENT, "probe stride (flags >> 20): 1, 2 or 4");
-    R->probe_stride = stride ? stride : 1;
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "probe stride (flags >> 20): 0, 1, 2 or 4");
+    R->probe_stride = stride;
     return CRT_OK;
 }
 
@@ -3460,7 +3434,6 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.ovf = nullptr;
     P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0; P.crit_tiles = 0; P.crit_threshold = 64;
     P.top_levels = R->top_levels < 0 ? CRT_TOP_LEVELS : R->top_levels;
-    P.reject_cap = R->reject_cap;
     P.carry_lanes = R->carry_lanes;
     P.carry_max = R->carry_max;
     P.stack_cap = S->stack_cap;
@@ -3558,13 +3531,17 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             Q.spp = probe_spp_for(R, spp);
             Q.accumulate = 0;
             Q.probe_cost = R->d_tile_cost;
-            Q.probe_stride = R->probe_stride;   // 1, 2 or 4: every stride-th pixel in x and y
-            const int ps = 16 * R->probe_stride;
+            // every stride-th pixel in x and y; automatic: 2 below 1000 spp, where the probe is a larger share of the
+            // frame (a 250-spp rank share: probe 3.2 -> 1.2 ms, render -0.9 %; at 2000 spp the render is unchanged,
+            // profiles/r04f)
+            const int pst = R->probe_stride ? R->probe_stride : (spp >= 1000 ? 1 : 2);
+            Q.probe_stride = pst;
+            const int ps = 16 * pst;
             const dim3 pgrid((R->width + ps - 1) / ps, (R->height + ps - 1) / ps);
             if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<true, 4, 6>), pgrid, block, 0, st, Q);
             else hipLaunchKernelGGL((crt_render_kernel<true, 4, 5>), pgrid, block, 0, st, Q);
             hipLaunchKernelGGL(crt_tile_cost_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_tile_cost,
-                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode, R->probe_stride);
+                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode, pst);
             if (R->tile_key_mode == 2) {   // per-pixel costs are no longer needed: reuse them for the smoothed keys
                 hipLaunchKernelGGL(crt_tile_neighbour_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st,
                                    R->d_tile_key, tiles_x, n_tiles, R->d_tile_cost);
@@ -3930,12 +3907,6 @@ int crt_renderer_timing_history(crt_renderer* R, int back, float out[3]) {
     HIP_TRY(hipEventElapsedTime(&out[0], slot[0], slot[2]));
     HIP_TRY(hipEventElapsedTime(&out[1], slot[0], slot[1]));
     HIP_TRY(hipEventElapsedTime(&out[2], slot[1], slot[2]));
-    return CRT_OK;
-}
-
-int crt_renderer_set_rejection_cap(crt_renderer* R, int candidates) {
-    if (!R || candidates < 0 || candidates > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "rejection cap in [0, 64]");
-    R->reject_cap = candidates;
     return CRT_OK;
 }
 

@@ -349,27 +349,6 @@ def test_xcd_regions_are_bit_identical(rebuilt, w, h, spp):
     assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1]) and out[0][2] == out[1][2]
 
 
-@pytest.mark.parametrize("cap", [1, 3])
-def test_rejection_cap_is_bit_identical(rebuilt, cap):
-    """Variant 8 with the unit-sphere rejection cap (crt_renderer_set_rejection_cap): a lane whose candidates all miss
-    waits for the next pass and continues its draws there, so frames, RNG state and ray counts equal the uncapped
-    frame bit for bit.  2560x1440 at 64 spp runs the probe, so the first 1,024 tiles (critical, never capped) and the
-    rest (capped) are both covered; cap 1 defers about half the Lambertian/Metal lanes of every pass."""
-    dev = rebuilt["cornell_bunny", "w4"]
-    w, h, spp = 2560, 1440, 64
-    out = []
-    for c in (0, cap):
-        r = crt_amd.Renderer(w, h)
-        r.set_rejection_cap(c)
-        r.set_camera(crt_amd.camera(spp))
-        r.init_rand(41)
-        r.render(dev, spp, 20)
-        r.synchronize()
-        assert r.last_kernel_name() == "crt_render_kernel<false, 8, 7>"
-        out.append((r.linear().view(np.uint32), r.rng_state(), r.counters()["rays"]))
-    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1]) and out[0][2] == out[1][2]
-
-
 @pytest.mark.parametrize("stride", [2, 4])
 def test_probe_stride_is_bit_identical(rebuilt, stride):
     """Variant 8 with a subsampled cost probe (every 2nd / 4th pixel in x and y): only the tile order changes, so the

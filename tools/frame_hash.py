@@ -20,8 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--big", action="store_true")
 ap.add_argument("--occupancy", type=int, default=0, help="crt_renderer_set_occupancy_target (0 = the library's default)")
 ap.add_argument("--xcd-regions", type=int, default=0, help="crt_renderer_set_xcd_regions (variant 8 tile order)")
-ap.add_argument("--rejection-cap", type=int, default=0, help="crt_renderer_set_rejection_cap (variant 8)")
-ap.add_argument("--probe-stride", type=int, default=1, help="variant 8's probe stride (crt_renderer_set_schedule)")
+ap.add_argument("--probe-stride", type=int, default=0, help="variant 8's probe stride (crt_renderer_set_schedule; 0 = auto)")
 a = ap.parse_args()
 
 hs = crt_amd.HostScene(assets.scene_files("cornell_bunny"), build_device=0)
@@ -39,9 +38,7 @@ for sc_name, w, h, spp, var, count in cases:
         r.set_occupancy_target(a.occupancy)
     if a.xcd_regions:
         r.set_xcd_regions(1)
-    if a.rejection_cap:
-        r.set_rejection_cap(a.rejection_cap)
-    if a.probe_stride != 1:
+    if a.probe_stride:
         r.set_schedule(-1, 64, probe_stride=a.probe_stride)
     r.set_camera(crt_amd.camera(spp))
     r.init_rand(41)

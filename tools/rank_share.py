@@ -31,7 +31,7 @@ ap.add_argument("--bounces", type=int, default=20)
 ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--all-ranks", type=int, default=8, help="also time every rank of this world size once")
-ap.add_argument("--probe-stride", type=int, default=1, help="variant 8's probe stride (crt_renderer_set_schedule)")
+ap.add_argument("--probe-stride", type=int, default=0, help="variant 8's probe stride (crt_renderer_set_schedule; 0 = auto)")
 a = ap.parse_args()
 
 W, H = a.width, a.height
@@ -39,7 +39,7 @@ hs = crt_amd.HostScene(assets.scene_files(a.scene), build_device=0)
 sc = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
 r = crt_amd.Renderer(W, H, 0)
 r.set_camera(crt_amd.camera(a.spp))
-if a.probe_stride != 1:
+if a.probe_stride:
     r.set_schedule(-1, 64, probe_stride=a.probe_stride)
 scale = crt_amd.pixel_sample_scale(a.spp)
 
