@@ -1,24 +1,37 @@
 #!/bin/bash
 # The current one-off GPU job (overwritten per job; the copy that ran is kept as profiles/<id>/job.sh).
-# r04z: round-4 final measurement set, part 2 at HEAD with the r04y counter summaries committed: the default bench and
-# configs B, E (parity + roofline) and A, the RCCL one-rank bench, rank shares, the interactive loop, 2 gloo ranks.
+# r04h: (1) the 4-wide kernels keep a ray's o and d in its LDS record only (in-tree) against HEAD's build (base): bits,
+# C and E A/B, the interactive loop; (2) the critical tiles' threshold re-swept on B, and C with the best of it.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=r04z; OUT=$R/gpurun_out/$O; mkdir -p $OUT
+O=r04h; OUT=$R/gpurun_out/$O; mkdir -p $OUT
 cd $R
-sha256sum raytracer-cuda_amd/csrc/crt_hip.hip raytracer-cuda_amd/lib/libcrt_hip.so > $OUT/sha.txt
-timeout -k 10 400 python3 bench.py --steps 5 > $OUT/bench.log 2>&1
-timeout -k 10 300 python3 bench.py --width 1280 --height 720 --spp 256 --steps 5 --no-cpu-baseline > $OUT/B.log 2>&1
-timeout -k 10 400 python3 bench.py --scene cornell_1m --spp 512 --steps 3 --no-cpu-baseline > $OUT/E.log 2>&1
-timeout -k 10 300 python3 bench.py --scene cornell --width 256 --height 256 --spp 16 --bounces 4 --steps 20 --cpu-threads 1 > $OUT/A.log 2>&1
-for f in bench B E A; do echo "$f: $(tail -1 $OUT/$f.log | cut -c1-160)"; done
-timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
-    --master-port 29514 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline --no-parity > $OUT/bench_rccl1.log 2>&1
-tail -1 $OUT/bench_rccl1.log | cut -c1-200
-timeout -k 10 300 python3 tools/rank_share.py > $OUT/rank_share.txt 2>&1
-timeout -k 10 300 python3 tools/section_profile.py --spp 256 > $OUT/section_C256.txt 2>&1
+sha256sum raytracer-cuda_amd/csrc/crt_hip.hip raytracer-cuda_amd/lib/libcrt_hip.so raytracer-cuda_amd/lib_exp/base/libcrt_hip.so > $OUT/sha.txt
+BASE=$R/raytracer-cuda_amd/lib_exp/base/libcrt_hip.so
+timeout -k 10 200 python3 tools/frame_hash.py --big > $OUT/hash_intree.txt 2>&1
+CRT_HIP_LIB=$BASE timeout -k 10 200 python3 tools/frame_hash.py --big > $OUT/hash_base.txt 2>&1
+cmp <(grep -v amdgpu.ids $OUT/hash_intree.txt) <(grep -v amdgpu.ids $OUT/hash_base.txt) && echo "o/d in LDS: hashes identical" || echo "o/d in LDS: HASHES DIFFER"
+B="python3 bench.py --no-cpu-baseline --no-count --no-parity"
+g() { grep -o '"render_ms": [0-9.]*, "probe_sort_ms": [0-9.]*, "main_kernel_ms": [0-9.]*' $1 | tail -1; }
+for i in 1 2 3; do
+  CRT_HIP_LIB=$BASE timeout -k 10 300 $B > $OUT/C_base_$i.log 2>&1
+  timeout -k 10 300 $B > $OUT/C_new_$i.log 2>&1
+  for f in C_base C_new; do echo "$f round $i: $(g $OUT/${f}_$i.log)"; done
+done
+for i in 1 2; do
+  CRT_HIP_LIB=$BASE timeout -k 10 300 $B --scene cornell_1m --spp 512 > $OUT/E_base_$i.log 2>&1
+  timeout -k 10 300 $B --scene cornell_1m --spp 512 > $OUT/E_new_$i.log 2>&1
+  for f in E_base E_new; do echo "$f round $i: $(g $OUT/${f}_$i.log)"; done
+done
 bash tools/gpu_job.sh viewer $O/viewer
-timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29515 bench.py --gpus 2 --steps 2 --warmup 1 --dist-backend gloo > $OUT/bench_2rank_gloo.log 2>&1
-tail -1 $OUT/bench_2rank_gloo.log | cut -c1-200
+for i in 1 2; do
+  for spec in "1024 16" "1024 24" "1024 32" "2048 24" "512 24" "1024 20"; do
+    set -- $spec; timeout -k 10 300 $B --width 1280 --height 720 --spp 256 --steps 5 --critical-tiles $1 --critical-lanes $2 > $OUT/B_c$1_l$2_$i.log 2>&1
+    echo "B crit $1 lanes $2 round $i: $(g $OUT/B_c$1_l$2_$i.log)"
+  done
+  for l in 16 24; do
+    timeout -k 10 300 $B --critical-tiles 1024 --critical-lanes $l > $OUT/C_l${l}_$i.log 2>&1
+    echo "C crit lanes $l round $i: $(g $OUT/C_l${l}_$i.log)"
+  done
+done
 echo job done
