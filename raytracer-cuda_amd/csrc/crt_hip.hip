@@ -683,11 +683,10 @@ __device__ __forceinline__ float4 node_row(const float4* __restrict__ nodes, uin
 __device__ __forceinline__ uint32_t sign_row(float inv) { return (__float_as_uint(inv) >> 27) & 16u; }
 // The ray's entry-row offsets for the three axes, one byte each (row 2a ^ sign, in 16-B units), computed once per
 // ray: a node step then needs one xor per row address instead of re-deriving the signs.
-__device__ __forceinline__ V3 ray_noi(V3 o, V3 inv) { return v3(-(o.x * inv.x), -(o.y * inv.y), -(o.z * inv.z)); }
 __device__ __forceinline__ uint32_t ray_rows(V3 inv) {
     return sign_row(inv.x) | ((32u ^ sign_row(inv.y)) << 8) | ((64u ^ sign_row(inv.z)) << 16);
 }
-__device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ nodes, uint32_t b, uint32_t rows, V3 noi, V3 inv,
+__device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ nodes, uint32_t b, uint32_t rows, V3 o, V3 inv,
                                             float tmax) {
     const uint32_t ex = b ^ (rows & 0xffu), ey = b ^ ((rows >> 8) & 0xffu), ez = b ^ (rows >> 16);
     const float4 nxr = *rec_at(nodes, ex), fxr = *rec_at(nodes, ex ^ 16u);
@@ -696,8 +695,7 @@ __device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ nodes, ui
     // one v_fma_f32 per plane: a v_pk_fma_f32 costs the SIMD the same cycles as two (MI355X_MICROARCH.md) and needs
     // {inv, inv} / {-o*inv, -o*inv} register pairs, which made the persistent variant 7 spill in this step (the
     // scalar form: variant 8 -1.7 %, variant 7 -18 %, profiles/r02aa)
-    // noi = -(o * inv), computed once per ray (ray_noi): the same operation the per-step form did, so the same bits
-    const float nx = noi.x, ny = noi.y, nz = noi.z;
+    const float nx = -(o.x * inv.x), ny = -(o.y * inv.y), nz = -(o.z * inv.z);
     Wide4 w;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -832,7 +830,7 @@ __device__ int trace4(const float4* __restrict__ nodes, const float4* __restrict
     int stack[64];
     while (node >= 0) {
         const uint32_t b = node_base(node);
-        const Wide4 w = wide_boxes(nodes, b, ray_rows(box_inv(inv)), ray_noi(o, box_inv(inv)), box_inv(inv), closest);
+        const Wide4 w = wide_boxes(nodes, b, ray_rows(box_inv(inv)), o, box_inv(inv), closest);
         const float4 mf = node_row(nodes, b, 6);
         const int first_child = __float_as_int(mf.x), n_int = __float_as_int(mf.y) & 0xff;
         const uint32_t counts = __float_as_uint(mf.w);
@@ -887,7 +885,7 @@ __device__ __forceinline__ int lane_fresh() {
 }
 
 template <bool COUNT>
-__device__ __forceinline__ void node_step4(const RenderParams& P, V3 noi, V3 inv, uint32_t rows, int& node, int& sp, float closest,
+__device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, uint32_t rows, int& node, int& sp, float closest,
                                            TraceCounts& cnt, uint32_t* __restrict__ stk, int lane, size_t pix,
                                            size_t n_pix, int& leaf_first, int& leaf_n) {
     leaf_n = 0;
@@ -895,7 +893,7 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 noi, V3 inv
     if (node >= 0) {
         const uint32_t b = node_base(node);
         const float4 mf = node_row(P.nodes, b, 6);
-        const Wide4 w = wide_boxes(P.nodes, b, rows, noi, inv, closest);
+        const Wide4 w = wide_boxes(P.nodes, b, rows, o, inv, closest);
         // keep the whole link row in the node's loads: left to itself the compiler loads leaf_first / counts
         // only inside the leaf branch, one more dependent load on a leaf step's critical path.  Pinned after the
         // box tests, so the wait it implies is the one the boxes need anyway (pinned before them, it made the six
@@ -969,13 +967,13 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 noi, V3 inv
 }
 
 template <bool COUNT>
-__device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 noi, V3 inv, uint32_t rows, int& node, int& sp,
+__device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
                                                float& closest, int& hit, TraceCounts& cnt, WaveLdsWide& L,
                                                uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix) {
     if (COUNT) cnt.step_slots++;
     const uint64_t c0 = COUNT ? shader_clock() : 0;
     int leaf_n, leaf_first;
-    node_step4<COUNT>(P, noi, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
+    node_step4<COUNT>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
     const uint64_t c1 = COUNT ? shader_clock() : 0;
     if (COUNT) cnt.cyc_step += c1 - c0;
 #ifdef CRT_PROFILE_PAIRS
@@ -996,7 +994,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 noi, V3
     {   // every lane writes its own slots, only the owners' are read: no branch (-0.8 %, profiles/r02ar)
         // leaf_first - prefix: a pair's primitive is ray1.w + its index j (-0.27 %, profiles/r02aq; round 1 measured
         // this +2.2 %, profiles/r01aj, before the round-2 changes to the round's code)
-        *reinterpret_cast<float2*>(&L.ray1[lane].z) = make_float2(closest, __int_as_float(leaf_first - pfx));
+        L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first - pfx));
 #ifdef CRT_CHECKED
         L.prefix[lane] = pfx;
         L.span_n[lane] = leaf_n;
@@ -1082,7 +1080,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 noi, V3
 //  * a lane's LDS key stays ~0 except while its span is being tested, and is reset when its span completes, so a
 //    partly tested span keeps its running min across steps.
 template <bool COUNT>
-__device__ __forceinline__ void traverse_step4c(const RenderParams& P, V3 noi, V3 inv, uint32_t rows, int& node, int& sp,
+__device__ __forceinline__ void traverse_step4c(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
                                                 float& closest, int& hit, uint32_t& pend, TraceCounts& cnt,
                                                 WaveLdsWide& L, uint32_t* __restrict__ stk, int lane, size_t pix,
                                                 size_t n_pix) {
@@ -1094,7 +1092,7 @@ __device__ __forceinline__ void traverse_step4c(const RenderParams& P, V3 noi, V
         leaf_first = (int)(pend >> 8);
         leaf_n = (int)(pend & 0xffu);
     } else {
-        node_step4<COUNT>(P, noi, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
+        node_step4<COUNT>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
     }
     const uint64_t c1 = COUNT ? shader_clock() : 0;
     if (COUNT) cnt.cyc_step += c1 - c0;
@@ -1109,7 +1107,7 @@ __device__ __forceinline__ void traverse_step4c(const RenderParams& P, V3 noi, V
     if (rem != 0 && !(limit >= total_c && rem <= P.carry_max &&
                       __popcll(wave_ballot(node >= 0)) >= P.carry_lanes))
         limit = total;                       // run the remainder now
-    *reinterpret_cast<float2*>(&L.ray1[lane].z) = make_float2(closest, __int_as_float(leaf_first - pfx));
+    L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first - pfx));
 #ifdef CRT_CHECKED
     L.prefix[lane] = pfx;
     L.span_n[lane] = leaf_n;
@@ -1215,14 +1213,14 @@ __device__ __forceinline__ void leaf_round4d(const RenderParams& P, WaveLdsWide&
 // offsets come from the owner lane's register through ds_bpermute) and the step's new one (offsets in the LDS ray
 // record).  Each step folds its per-owner minimum into (closest, hit) and clears the key.
 template <bool COUNT>
-__device__ __forceinline__ void traverse_step4d(const RenderParams& P, V3 noi, V3 inv, uint32_t rows, int& node, int& sp,
+__device__ __forceinline__ void traverse_step4d(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
                                                 float& closest, int& hit, uint32_t& pend, TraceCounts& cnt,
                                                 WaveLdsWide& L, uint32_t* __restrict__ stk, int lane, size_t pix,
                                                 size_t n_pix) {
     if (COUNT) cnt.step_slots++;
     const uint64_t c0 = COUNT ? shader_clock() : 0;
     int leaf_n, leaf_first;
-    node_step4<COUNT>(P, noi, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
+    node_step4<COUNT>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
     const uint64_t c1 = COUNT ? shader_clock() : 0;
     if (COUNT) cnt.cyc_step += c1 - c0;
     const int cn = (int)(pend & 0xffu);
@@ -1237,7 +1235,7 @@ __device__ __forceinline__ void traverse_step4d(const RenderParams& P, V3 noi, V
     if (rem != 0 && !(limit >= total_c && rem <= P.carry_max &&
                       __popcll(wave_ballot(node >= 0)) >= P.carry_lanes))
         limit = total;
-    *reinterpret_cast<float2*>(&L.ray1[lane].z) = make_float2(closest, __int_as_float(leaf_first - pfx));
+    L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first - pfx));
     {
         uint32_t ones;
         __asm__ volatile("v_mov_b32 %0, -1" : "=v"(ones));
@@ -1278,10 +1276,10 @@ constexpr int TOP_NODES = CRT_TOP_LEVELS >= 2 ? 5 : CRT_TOP_LEVELS >= 1 ? 1 : 0;
 // false, changing nothing, when a leaf child is hit: the lane then takes this node through the regular step, whose
 // leaf rounds test it.
 template <bool COUNT>
-__device__ __forceinline__ bool top_step4(const RenderParams& P, const float4* rec, V3 noi, V3 inv, uint32_t rows,
+__device__ __forceinline__ bool top_step4(const RenderParams& P, const float4* rec, V3 o, V3 inv, uint32_t rows,
                                           int& node, int& sp, TraceCounts& cnt, uint32_t* __restrict__ stk,
                                           size_t pix, size_t n_pix) {
-    const Wide4 w = wide_boxes(rec, 0u, rows, noi, inv, __builtin_inff());
+    const Wide4 w = wide_boxes(rec, 0u, rows, o, inv, __builtin_inff());
     const float4 mf = rec[6];
     const int first_child = __float_as_int(mf.x);
     const int meta = __float_as_int(mf.y);
@@ -1323,15 +1321,15 @@ __device__ __forceinline__ bool top_step4(const RenderParams& P, const float4* r
 
 // A new ray's first node steps from the LDS top nodes: the root, then (TOPN = 5) the internal child it continues to.
 template <bool COUNT, int TOPN>
-__device__ __forceinline__ void top_steps(const RenderParams& P, const float4* top, V3 noi, V3 inv, uint32_t rows,
+__device__ __forceinline__ void top_steps(const RenderParams& P, const float4* top, V3 o, V3 inv, uint32_t rows,
                                           int& node, int& sp, TraceCounts& cnt, uint32_t* __restrict__ stk, size_t pix,
                                           size_t n_pix) {
     if (P.top_levels <= 0) return;   // uniform
-    if (!top_step4<COUNT>(P, top, noi, inv, rows, node, sp, cnt, stk, pix, n_pix) || TOPN < 5 || P.top_levels < 2 ||
+    if (!top_step4<COUNT>(P, top, o, inv, rows, node, sp, cnt, stk, pix, n_pix) || TOPN < 5 || P.top_levels < 2 ||
         node < 0)
         return;
     const int m = node - __float_as_int(top[6].x);   // node is an internal child of the root: slot m < 4
-    if ((unsigned)m < 4u) top_step4<COUNT>(P, top + 8 * (1 + m), noi, inv, rows, node, sp, cnt, stk, pix, n_pix);
+    if ((unsigned)m < 4u) top_step4<COUNT>(P, top + 8 * (1 + m), o, inv, rows, node, sp, cnt, stk, pix, n_pix);
 }
 
 // Per-lane path state of one pixel (rayColor's locals, CUDAKernels.h:102-145, plus the sample loop).
@@ -1507,20 +1505,6 @@ __device__ __forceinline__ void shade_rec(PathState& S, const RenderParams& P, i
     }
 }
 
-// The 4-wide variants keep a ray's origin and direction in its LDS record only (ray0 = o.xyz, d.x; ray1 = d.y, d.z,
-// then the step's closest and primitive offset), so they are not live in registers across the traversal steps: the
-// steps need only -(o * inv) (ray_noi), and the regeneration pass reloads o and d for its parked lanes.
-__device__ __forceinline__ void store_ray(const PathState& S, WaveLdsWide& L, int lane) {
-    L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
-    *reinterpret_cast<float2*>(&L.ray1[lane]) = make_float2(S.d.y, S.d.z);
-}
-__device__ __forceinline__ void load_ray(PathState& S, const WaveLdsWide& L, int lane) {
-    const float4 a = L.ray0[lane];
-    const float2 b = *reinterpret_cast<const float2*>(&L.ray1[lane]);
-    S.o = v3(a.x, a.y, a.z);
-    S.d = v3(a.w, b.x, b.y);
-}
-
 // A parked lane's end of trace in the regeneration pass (4-wide variants): the per-ray spheres (Sphere::hit behind the
 // reference's sphere box, ray_spheres) and then shade.  The trace's own hit record is loaded before the sphere test,
 // behind a compiler barrier, so its latency hides behind that test (-0.6 %, profiles/r03aa); when a per-ray sphere
@@ -1688,7 +1672,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         bool live = false, has_result = false, have = false;
         int node = -1, sp = 0, hit = -1, px = 0, py = 0, ppix = 0;
         float closest = INF;
-        V3 inv = v3(0.f, 0.f, 0.f), noi = inv;   // noi = ray_noi(o, inv): the ray's o and d live in its LDS record
+        V3 inv = v3(0.f, 0.f, 0.f);
         uint32_t rows = 0;         // ray_rows(inv)
         uint32_t pool = 0, used = 64;    // wave-uniform: first slot of the reserved block, slots handed out
         bool exhausted = false;
@@ -1701,10 +1685,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             if (n_parked >= P.regen_threshold || n_parked == n_live) {
                 if (COUNT) cnt.passes++;
                 if (parked) {
-                    if (has_result) {
-                        load_ray(S, L, lane);
-                        finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, c0);
-                    }
+                    if (has_result) finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, c0);
                     live = next_ray(S, C, px, py, P.max_bounces);
                     has_result = false;
                 }
@@ -1765,16 +1746,15 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     inv = recip3_exact(S.d);
                     inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
                     rows = ray_rows(inv);
-                    noi = ray_noi(S.o, inv);
                     if (COUNT) cnt.spheres += P.n_ray_spheres;
-                    store_ray(S, L, lane);
+                    L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                     if (COUNT) cnt.trace_calls++;
-                    if (TOPN > 0) top_steps<COUNT, TOPN>(P, top_lds, noi, inv, rows, node, sp, cnt, stk, (size_t)ppix, n_pix);
+                    if (TOPN > 0) top_steps<COUNT, TOPN>(P, top_lds, S.o, inv, rows, node, sp, cnt, stk, (size_t)ppix, n_pix);
                 }
                 if (!wave_ballot(live)) break;      // the queue is empty and every lane is done
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
-            traverse_step4<COUNT>(P, noi, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)ppix, n_pix);
+            traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)ppix, n_pix);
         }
     } else if constexpr (WIDE) {
         // Same scheduling as variant 3 over a 4-wide BVH: node < 0 = no node left (lane parked).
@@ -1789,7 +1769,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         bool has_result = false;
         int node = -1, sp = 0, hit = -1;
         float closest = INF;
-        V3 inv = v3(0.f, 0.f, 0.f), noi = inv;   // noi = ray_noi(o, inv): the ray's o and d live in its LDS record
+        V3 inv = v3(0.f, 0.f, 0.f);
         uint32_t rows = 0;         // ray_rows(inv)
         L.owner_at[lane] = 0;      // traverse_step4: owner + 1, 0 = none
         if (TILED && lane == 0) L.rays = 0;
@@ -1817,7 +1797,6 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     // the lanes with a ray): a uniform test instead of a divergent branch on has_result (-0.38 %,
                     // profiles/r02av)
                     if (!first_pass) {
-                        load_ray(S, L, lane);
                         finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, s0);
                     }
                     const uint64_t s1 = COUNT ? shader_clock() : 0;
@@ -1840,11 +1819,10 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         inv = recip3_exact(S.d);
                         inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
                         rows = ray_rows(inv);
-                        noi = ray_noi(S.o, inv);
                         if (COUNT) cnt.spheres += P.n_ray_spheres;
-                        store_ray(S, L, lane);
+                        L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                         if (COUNT) cnt.trace_calls++;
-                        if (TOPN > 0) top_steps<COUNT, TOPN>(P, top_lds, noi, inv, rows, node, sp, cnt, stk, (size_t)pix, n_pix);
+                        if (TOPN > 0) top_steps<COUNT, TOPN>(P, top_lds, S.o, inv, rows, node, sp, cnt, stk, (size_t)pix, n_pix);
                     }
                 }
                 live_mask = wave_ballot(has_result);
@@ -1854,13 +1832,13 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
             if constexpr (CARRY && CRT_LEAF_CARRY == 2)
-                traverse_step4d<COUNT>(P, noi, inv, rows, node, sp, closest, hit, pend, cnt, L, stk, lane,
+                traverse_step4d<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, pend, cnt, L, stk, lane,
                                        (size_t)pix, n_pix);
             else if constexpr (CARRY)
-                traverse_step4c<COUNT>(P, noi, inv, rows, node, sp, closest, hit, pend, cnt, L, stk, lane,
+                traverse_step4c<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, pend, cnt, L, stk, lane,
                                        (size_t)pix, n_pix);
             else
-                traverse_step4<COUNT>(P, noi, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix,
+                traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix,
                                       n_pix);
         }
     } else if constexpr (VARIANT == 2 || VARIANT == 3 || VARIANT == 10) {
