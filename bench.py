@@ -303,7 +303,8 @@ def main():
     torch.cuda.set_device(local)
     # a process group whenever torch.distributed.run launched us, even with one rank: `--nproc-per-node 1` then runs
     # the production collective path (RCCL reduce of the framebuffer on a one-rank communicator) on a single GPU
-    launched = "TORCHELASTIC_RUN_ID" in os.environ or "MASTER_ADDR" in os.environ
+    launched = "TORCHELASTIC_RUN_ID" in os.environ or all(
+        k in os.environ for k in ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE"))
     grouped = world > 1 or launched
     if grouped:
         if args.dist_backend == "nccl":
