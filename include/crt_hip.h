@@ -273,6 +273,11 @@ int  crt_renderer_set_top_levels(crt_renderer* r, int levels);
  * and carries a part-empty remainder of at most `max_pairs` (0..63; 0 = never) pairs to the next step when at least
  * `lanes` (0..64; 65 = never) lanes are still traversing.  Results never depend on it. */
 int  crt_renderer_set_leaf_carry(crt_renderer* r, int lanes, int max_pairs);
+/* Variant 7 without the cost probe (the interactive loop's 1-spp frames): 1 = dispatch its 8x8 tiles most expensive
+ * first by the rays per pixel the previous variant-7 render of this renderer counted (consecutive frames share the cost
+ * map; the first frame, and any after this call, use row order); 0 = row order (default for the renderer; the
+ * CRT::Raytracer loop turns it on).  Results never depend on it. */
+int  crt_renderer_set_temporal_order(crt_renderer* r, int on);
 /* Variant 8 with the cost probe: 1 = the blocks that share an XCD (block index mod 8, MI355X's round-robin dispatch)
  * render one screen strip of equal probe cost, most expensive tile first, so each XCD's L2 holds its strip's geometry;
  * 0 = one global cost order (default).  Ignored with pixel sharding.  Results never depend on it. */

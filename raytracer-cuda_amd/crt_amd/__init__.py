@@ -309,6 +309,10 @@ class Renderer:
         check(_lib.hip().crt_renderer_last_timings(self.h, a), "last_timings")
         return {"render_ms": float(a[0]), "probe_sort_ms": float(a[1]), "main_kernel_ms": float(a[2])}
 
+    def set_temporal_order(self, on: bool):
+        """Variant 7: tiles most expensive first by the previous frame's rays per pixel (crt_renderer_set_temporal_order)."""
+        check(_lib.hip().crt_renderer_set_temporal_order(self.h, int(bool(on))), "set_temporal_order")
+
     def set_xcd_regions(self, on: bool):
         """Variant 8: XCD groups render equal-cost screen strips (crt_renderer_set_xcd_regions)."""
         check(_lib.hip().crt_renderer_set_xcd_regions(self.h, int(bool(on))), "set_xcd_regions")

@@ -77,6 +77,7 @@ struct RenderParams {
     int tiles_x;                          // variant 8: 8x8 tiles per row (order[] holds tile indices)
     uint32_t* __restrict__ probe_cost;    // probe launch (variant 4): rays per pixel; nothing else is written
     int probe_stride;                     // probe launch (variant 4): lanes take every probe_stride-th pixel in x and y
+    uint32_t* __restrict__ pix_rays;      // variant 7: rays each pixel took this frame (the next frame's tile order)
     int crit_tiles, crit_threshold;       // variant 8: the first crit_tiles tiles of the cost order regenerate at
                                           // crit_threshold parked lanes instead of regen_threshold
     int top_levels;                       // 4-wide variants: a new ray's first node steps taken from LDS (<= CRT_TOP_LEVELS)
@@ -1577,6 +1578,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     // reads the record from LDS (the trace's own hit record is loaded at the pass start)
     __shared__ float4 shd_lds[WIDE ? 6 : 1];
     __shared__ float4 top_lds[TOPN > 0 ? 8 * TOPN : 1];   // CRT_TOP_LEVELS: root, then its internal children
+    __shared__ uint32_t rays0_lds[PERSIST ? 64 * WGW : 1];   // variant 7: the lane's ray count when its pixel started
 #ifdef CRT_LDS_PAD
     __shared__ float4 pad_lds[CRT_LDS_PAD / 16];          // experiment: LDS footprint alone
     __asm__ volatile("" : : "v"(&pad_lds[threadIdx.x & 1]));
@@ -1695,6 +1697,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     P.sum[3 * (size_t)ppix] = S.pixel.x;
                     P.sum[3 * (size_t)ppix + 1] = S.pixel.y;
                     P.sum[3 * (size_t)ppix + 2] = S.pixel.z;
+                    if (P.pix_rays) P.pix_rays[ppix] = S.rays - rays0_lds[threadIdx.x];
                     have = false;
                 }
                 while (!exhausted) {                // lanes without a pixel take the next slots
@@ -1723,6 +1726,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                             S.remaining = P.spp;
                             S.need_new = true;
                             have = true;
+                            rays0_lds[threadIdx.x] = S.rays;
                             live = next_ray(S, C, px, py, P.max_bounces);
                             if (!live) {         // spp == 0: nothing to trace, store as is
                                 uint32_t* w = P.rng + 6 * (size_t)ppix;
@@ -1730,6 +1734,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                                 P.sum[3 * (size_t)ppix] = S.pixel.x;
                                 P.sum[3 * (size_t)ppix + 1] = S.pixel.y;
                                 P.sum[3 * (size_t)ppix + 2] = S.pixel.z;
+                                if (P.pix_rays) P.pix_rays[ppix] = 0;
                                 have = false;
                             }
                         }
@@ -2402,6 +2407,16 @@ __global__ void crt_shard_tiles_kernel(uint32_t* __restrict__ order, int n_tiles
     if (k * shards + shard < n_tiles) order[k] = (uint32_t)(k * shards + shard);
 }
 
+// Variant 7 with the temporal order (crt_renderer_set_temporal_order): slots of 8x8 tiles in the order tile_order
+// holds (the tiles most expensive first by the previous frame's rays per pixel), pixels row-major inside a tile.
+__global__ void crt_expand_tile_order_kernel(const uint32_t* __restrict__ tile_order, uint32_t* __restrict__ order,
+                                             int width, int height, int n_slots) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_slots) return;
+    const int tiles_x = (width + 7) / 8, tile = (int)tile_order[s >> 6], q = s & 63;
+    const int x = (tile % tiles_x) * 8 + (q & 7), y = (tile / tiles_x) * 8 + (q >> 3);
+    order[s] = (x < width && y < height) ? (uint32_t)(y * width + x) : 0xffffffffu;
+}
 __global__ void crt_order_tiles_kernel(uint32_t* __restrict__ order, int width, int height, int n_slots) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_slots) return;
@@ -2925,6 +2940,10 @@ struct crt_renderer {
     int carry_lanes = 16, carry_max = 63;   // variant 8 leaf-pair carry (builds with CRT_LEAF_CARRY)
     int xcd_regions = 0;           // variant 8: XCD groups render screen strips (crt_xcd_order_kernel)
     int probe_stride = 0;          // variant 8's cost probe: every probe_stride-th pixel in x and y (0 = automatic)
+    int temporal = 0;              // variant 7: tiles ordered by the previous variant-7 frame's rays per pixel
+    uint32_t* d_pix_rays = nullptr;   // variant 7 with the temporal order: rays per pixel of the last frame
+    uint32_t* d_tile_order = nullptr; // its tiles, most expensive first
+    bool pix_rays_valid = false;
     int min_waves = 0;             // occupancy target (waves/SIMD); 0 = auto: 7 for variant 8 over >= 4 tiles per wave
                                    // slot, 6 for the other 4-wide launches and variants 3 and 10, 5 for variants 0-2
     uint32_t* d_ovf = nullptr;     // variant 4: stack entries beyond the LDS part, ovf_entries x W*H
@@ -3298,6 +3317,8 @@ void crt_renderer_destroy(crt_renderer* R) {
     if (R->d_tile_cost) (void)hipFree(R->d_tile_cost);
     if (R->d_order_hist) (void)hipFree(R->d_order_hist);
     if (R->d_tile_key) (void)hipFree(R->d_tile_key);
+    if (R->d_pix_rays) (void)hipFree(R->d_pix_rays);
+    if (R->d_tile_order) (void)hipFree(R->d_tile_order);
     if (R->d_rng_cache) (void)hipFree(R->d_rng_cache);
     for (auto& slot : R->ring)
         for (hipEvent_t& ev : slot)
@@ -3431,6 +3452,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     P.rcp_w = R->rcp_w; P.rcp_h = R->rcp_h; P.fast_uv = R->fast_uv;
     P.probe_stride = 1;
+    P.pix_rays = nullptr;
     P.ovf = nullptr;
     P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0; P.crit_tiles = 0; P.crit_threshold = 64;
     P.top_levels = R->top_levels < 0 ? CRT_TOP_LEVELS : R->top_levels;
@@ -3615,9 +3637,40 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
                                R->d_order_hist, R->d_order, 0u);
             P.n_slots = (int)n_pix;
         } else {
-            hipLaunchKernelGGL(crt_order_tiles_kernel, dim3((unsigned)((n_tile_slots + 255) / 256)), dim3(256), 0, st,
-                               R->d_order, R->width, R->height, (int)n_tile_slots);
+            const int n_tiles = tiles_x * tiles_y;
+            if (R->temporal && !R->d_pix_rays) {
+                HIP_TRY(hipStreamSynchronize(st));
+                HIP_TRY(hipMalloc((void**)&R->d_pix_rays, n_pix * 4));
+                HIP_TRY(hipMalloc((void**)&R->d_tile_order, (size_t)n_tiles * 4));
+                if (!R->d_tile_key) HIP_TRY(hipMalloc((void**)&R->d_tile_key, (size_t)n_tiles * 4));
+                R->pix_rays_valid = false;
+            }
+            if (R->temporal && R->pix_rays_valid) {
+                // the interactive loop's frames repeat the last frame's cost map: its rays per pixel -> tile keys (the
+                // slowest pixel, raised to 3/4 of the neighbours', as variant 8's probe keys) -> tiles most expensive
+                // first, so the long paths start early and the launch does not end with them (profiles/r04i: a 1-spp
+                // frame in row order spends its last 31 % draining)
+                hipLaunchKernelGGL(crt_tile_cost_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_pix_rays,
+                                   R->width, R->height, tiles_x, n_tiles, R->d_tile_order, 0, 1);
+                hipLaunchKernelGGL(crt_tile_neighbour_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st,
+                                   R->d_tile_order, tiles_x, n_tiles, R->d_tile_key);
+                const unsigned ob = (unsigned)((n_tiles + ORDER_ITEMS - 1) / ORDER_ITEMS);
+                HIP_TRY(hipMemsetAsync(R->d_order_hist, 0, ORDER_KEYS * 4, st));
+                hipLaunchKernelGGL(crt_order_hist_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key, n_tiles, R->d_order_hist);
+                hipLaunchKernelGGL(crt_order_scan_kernel, dim3(1), dim3(ORDER_KEYS), 0, st, R->d_order_hist);
+                hipLaunchKernelGGL(crt_order_scatter_kernel, dim3(ob), dim3(256), 0, st, R->d_tile_key, n_tiles,
+                                   R->d_order_hist, R->d_tile_order, 0u);
+                hipLaunchKernelGGL(crt_expand_tile_order_kernel, dim3((unsigned)((n_tile_slots + 255) / 256)), dim3(256),
+                                   0, st, R->d_tile_order, R->d_order, R->width, R->height, (int)n_tile_slots);
+            } else {
+                hipLaunchKernelGGL(crt_order_tiles_kernel, dim3((unsigned)((n_tile_slots + 255) / 256)), dim3(256), 0, st,
+                                   R->d_order, R->width, R->height, (int)n_tile_slots);
+            }
             P.n_slots = (int)n_tile_slots;
+            if (R->temporal) {
+                P.pix_rays = R->d_pix_rays;
+                R->pix_rays_valid = true;
+            }
         }
         HIP_TRY(hipMemsetAsync(R->d_queue, 0, 4, st));
         P.order = R->d_order;
@@ -3751,6 +3804,7 @@ int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene*
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     P.rcp_w = R->rcp_w; P.rcp_h = R->rcp_h; P.fast_uv = R->fast_uv;
     P.probe_stride = 1;
+    P.pix_rays = nullptr;
     Q.nodes_b = B->d_nodes; Q.prims_b = B->d_prims; Q.n_nodes_b = B->n_nodes; Q.n_layouts_b = B->layouts;
     Q.width_a = A->width; Q.width_b = B->width;
     Q.dump = nullptr;
@@ -3907,6 +3961,13 @@ int crt_renderer_timing_history(crt_renderer* R, int back, float out[3]) {
     HIP_TRY(hipEventElapsedTime(&out[0], slot[0], slot[2]));
     HIP_TRY(hipEventElapsedTime(&out[1], slot[0], slot[1]));
     HIP_TRY(hipEventElapsedTime(&out[2], slot[1], slot[2]));
+    return CRT_OK;
+}
+
+int crt_renderer_set_temporal_order(crt_renderer* R, int on) {
+    if (!R || on < 0 || on > 1) return set_error(CRT_ERR_INVALID_ARGUMENT, "temporal order: 0 or 1");
+    R->temporal = on;
+    R->pix_rays_valid = false;
     return CRT_OK;
 }
 

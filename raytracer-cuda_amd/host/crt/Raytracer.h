@@ -36,6 +36,9 @@ struct RaytracerOptions {
     float focusDist = 0.f;                  // <= 0: |position - (0,0,0)|, the reference's rule
     bool accumulate = false;
     int meshBuildDevice = -1;              // >= 0: mesh BVHs built on that GPU (same trees, SceneManager)
+    // variant 7 (the < 64-spp frames of the loop) dispatches its tiles most expensive first by the previous frame's rays
+    // per pixel (crt_renderer_set_temporal_order): consecutive frames share the cost map; results never depend on it
+    bool temporalOrder = true;
 };
 
 struct FrameInfo {
@@ -57,6 +60,7 @@ public:
           m_Aperture(aperture), m_Options(opts), m_SceneManager(width, height, opts.device),
           m_Renderer(width, height, opts.device) {
         initializeScene();
+        CRT_CHECK(crt_renderer_set_temporal_order(m_Renderer.handle(), opts.temporalOrder ? 1 : 0));
     }
 
     // Raytracer::updateAndRender (Raytracer.h:94-102) for one frame of input.

@@ -3,7 +3,7 @@
 // frame times are reported (the reference throttles to 60 fps; here frames run back to back).
 //
 //   crt_viewer [-w W] [-h H] [-frames N] [-script still|walk|orbit|hq] [-bvh reference|rebuilt]
-//              [-accumulate] [-seed S] [-o last.png] model.obj...
+//              [-accumulate] [-no-temporal] [-seed S] [-o last.png] model.obj...
 //
 // Scripts: still = no input (1 spp per frame, RNG continues); walk = W held; orbit = right mouse dragged
 // in a circle; hq = F pressed once, then still (2000 spp frames).
@@ -36,6 +36,7 @@ int main(int argc, char** argv) {
             else if (a == "-seed") { need(1); opts.seed = std::strtoull(argv[++i], nullptr, 10); }
             else if (a == "-o") { need(1); out = argv[++i]; }
             else if (a == "-accumulate") opts.accumulate = true;
+            else if (a == "-no-temporal") opts.temporalOrder = false;
             else if (a == "-bvh") {
                 need(1);
                 std::string m = argv[++i];
