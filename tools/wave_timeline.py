@@ -77,4 +77,26 @@ out = {"scene": a.scene, "bvh": a.bvh, "variant": a.variant, "temporal": a.tempo
        "wave_ms": {"min": round(float(dur.min()) / 1e3, 3), "median": round(float(np.median(dur)) / 1e3, 3),
                    "max": round(float(dur.max()) / 1e3, 3)},
        "resident_waves_per_twentieth": occ}
+if a.variant == 8:
+    # variant 8 runs block b on the b-th tile of the cost order, so the waves' durations in block order show how well
+    # the probe ranked the tiles.  Greedy list schedules over `peak` slots (a slot takes the next block when it frees):
+    # in block order (checks the model against the measured span) and in the order of the measured durations (the
+    # span a perfect cost probe would give).
+    import heapq
+
+    def list_schedule(d):
+        slots = [0.0] * peak
+        for x in d:
+            heapq.heapreplace(slots, slots[0] + x)
+        return max(slots)
+
+    tail = np.nonzero(end > steady_end)[0]
+    out["order"] = {"model_span_ms_block_order": round(list_schedule(dur) / 1e3, 3),
+                    "model_span_ms_true_lpt": round(list_schedule(np.sort(dur)[::-1]) / 1e3, 3),
+                    "tail_waves": int(len(tail)),
+                    "tail_block_quantiles": [round(float(q) / n_waves, 4) for q in
+                                             np.quantile(tail, [0.1, 0.5, 0.9])] if len(tail) else [],
+                    "tail_wave_ms_median": round(float(np.median(dur[tail])) / 1e3, 3) if len(tail) else 0.0,
+                    "last_ending_blocks": [int(b) for b in np.argsort(end)[-8:][::-1]],
+                    "wave_ms_by_block_decile": [round(float(np.median(x)) / 1e3, 3) for x in np.array_split(dur, 10)]}
 print(json.dumps(out))
