@@ -1,38 +1,25 @@
 #!/bin/bash
 # The current one-off GPU job (overwritten per job; the copy that ran is kept as profiles/<id>/job.sh).
-# r04j: the temporal tile order for variant 7 (the interactive loop's 1-spp frames): bits, wave timelines with and
-# without it, the interactive loop with and without it; variant 8 against HEAD's build (base) as a check.
+# r04k: final measurement set, part 1, at HEAD (crt_hip.hip with the temporal tile order): GPU suite, frame hashes,
+# smoke, PMC passes for configs C, B and E summarised on the box (so this job's bench line carries current counters),
+# the default bench (CPU baseline + parity) and the rocprofv3 kernel stats of the bench.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=r04j; OUT=$R/gpurun_out/$O; mkdir -p $OUT
+O=r04k; OUT=$R/gpurun_out/$O; mkdir -p $OUT
 cd $R
-sha256sum raytracer-cuda_amd/csrc/crt_hip.hip raytracer-cuda_amd/lib/libcrt_hip.so raytracer-cuda_amd/lib_exp/*/libcrt_hip.so > $OUT/sha.txt
-BASE=$R/raytracer-cuda_amd/lib_exp/base/libcrt_hip.so
-WT=$R/raytracer-cuda_amd/lib_exp/wavetimes/libcrt_hip.so
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_viewer.py -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest_viewer.log 2>&1
-tail -1 $OUT/pytest_viewer.log
-timeout -k 10 200 python3 tools/frame_hash.py --big > $OUT/hash_intree.txt 2>&1
-CRT_SKIP_ABI_CHECK=1 CRT_HIP_LIB=$BASE timeout -k 10 200 python3 tools/frame_hash.py --big > $OUT/hash_base.txt 2>&1
-cmp <(grep -v amdgpu.ids $OUT/hash_intree.txt) <(grep -v amdgpu.ids $OUT/hash_base.txt) && echo "hashes identical" || echo "HASHES DIFFER"
-for t in "" "--temporal" "" "--temporal"; do
-  CRT_HIP_LIB=$WT timeout -k 10 120 python3 tools/wave_timeline.py --variant 7 --spp 1 $t >> $OUT/timeline.jsonl 2>> $OUT/timeline.err
-done
-python3 -c "
-import json
-for l in open('$OUT/timeline.jsonl'):
-    d=json.loads(l); print(d['temporal'], d['kernel_ms'], d['span_ms'], d['occupancy_efficiency'], d['tail_ms'])"
-F=$(CRT_NO_TORCH=1 python3 -c "import sys; sys.path.insert(0, 'raytracer-cuda_amd'); from crt_amd import assets; print(' '.join(map(str, assets.scene_files('cornell_bunny'))))")
-for i in 1 2; do
-  for s in still orbit; do
-    timeout -k 10 120 raytracer-cuda_amd/bin/crt_viewer -frames 600 -script $s -bvh rebuilt $F > $OUT/viewer_${s}_temporal_$i.json
-    timeout -k 10 120 raytracer-cuda_amd/bin/crt_viewer -frames 600 -script $s -bvh rebuilt -no-temporal $F > $OUT/viewer_${s}_row_$i.json
-    echo "$s round $i: temporal $(grep -o '"fps": [0-9.]*' $OUT/viewer_${s}_temporal_$i.json), row $(grep -o '"fps": [0-9.]*' $OUT/viewer_${s}_row_$i.json)"
-  done
-done
-B="python3 bench.py --no-cpu-baseline --no-count --no-parity"
-for i in 1 2; do
-  CRT_SKIP_ABI_CHECK=1 CRT_HIP_LIB=$BASE timeout -k 10 300 $B > $OUT/C_base_$i.log 2>&1
-  timeout -k 10 300 $B > $OUT/C_new_$i.log 2>&1
-  for f in C_base C_new; do echo "$f round $i: $(grep -o '"main_kernel_ms": [0-9.]*' $OUT/${f}_$i.log | tail -1)"; done
-done
+sha256sum raytracer-cuda_amd/csrc/crt_hip.hip raytracer-cuda_amd/lib/libcrt_hip.so bench.py > $OUT/sha.txt
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+tail -1 $OUT/pytest_gpu.log
+timeout -k 10 180 python3 tools/frame_hash.py --big > $OUT/hash_intree.txt 2>&1
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+bash tools/pmc.sh gpurun_out/$O/pmc
+bash tools/pmc.sh gpurun_out/$O/pmc_B --width 1280 --height 720 --spp 256
+bash tools/pmc.sh gpurun_out/$O/pmc_E --scene cornell_1m --spp 512
+for p in pmc pmc_B pmc_E; do python3 tools/pmc_summary.py gpurun_out/$O/$p profiles/$O/$p > $OUT/summary_$p.log 2>&1; done
+cp profiles/roofline_counters.json $OUT/roofline_counters.json
+timeout -k 10 400 python3 bench.py --steps 5 > $OUT/bench.log 2>&1
+tail -1 $OUT/bench.log | cut -c1-200
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- \
+    python3 $R/bench.py --no-cpu-baseline --no-parity --steps 3 > $OUT/bench_prof.log 2>&1
 echo job done
