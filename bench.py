@@ -108,6 +108,8 @@ def parse():
     ap.add_argument("--critical-tiles", type=int, default=None,
                     help="variant 8: leading tiles of the cost order that regenerate sooner (default: library's)")
     ap.add_argument("--critical-lanes", type=int, default=16, help="their regeneration threshold")
+    ap.add_argument("--drain-threshold", type=int, default=None,
+                    help="variant 7: regeneration threshold once the pixel queue is empty (0 = unchanged)")
     ap.add_argument("--carry", type=int, nargs=2, default=None, metavar=("LANES", "MAX_PAIRS"),
                     help="variant 8 leaf-pair carry (crt_renderer_set_leaf_carry; CRT_LEAF_CARRY builds)")
     ap.add_argument("--xcd-regions", type=int, default=None, choices=[0, 1],
@@ -375,6 +377,8 @@ def main():
         r.set_leaf_carry(*args.carry)
     if args.xcd_regions is not None:
         r.set_xcd_regions(args.xcd_regions)
+    if args.drain_threshold is not None:
+        r.set_drain_threshold(args.drain_threshold)
     r.set_camera(cam)
     fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard,
                               collective=grouped)

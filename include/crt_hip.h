@@ -278,6 +278,10 @@ int  crt_renderer_set_leaf_carry(crt_renderer* r, int lanes, int max_pairs);
  * map; the first frame, and any after this call, use row order); 0 = row order (default for the renderer; the
  * CRT::Raytracer loop turns it on).  Results never depend on it. */
 int  crt_renderer_set_temporal_order(crt_renderer* r, int on);
+/* Variant 7 (frames below 64 spp): once its pixel queue is empty, a wave only drains, and its last paths' passes run
+ * at `lanes` parked lanes (1..64) instead of the regeneration threshold, so they wait less for each other; 0 = the
+ * regeneration threshold (the default).  Results never depend on it. */
+int  crt_renderer_set_drain_threshold(crt_renderer* r, int lanes);
 /* Variant 8 with the cost probe: 1 = the blocks that share an XCD (block index mod 8, MI355X's round-robin dispatch)
  * render one screen strip of equal probe cost, most expensive tile first, so each XCD's L2 holds its strip's geometry;
  * 0 = one global cost order (default).  Ignored with pixel sharding.  Results never depend on it. */

@@ -313,6 +313,10 @@ class Renderer:
         """Variant 7: tiles most expensive first by the previous frame's rays per pixel (crt_renderer_set_temporal_order)."""
         check(_lib.hip().crt_renderer_set_temporal_order(self.h, int(bool(on))), "set_temporal_order")
 
+    def set_drain_threshold(self, lanes: int):
+        """Variant 7: regeneration threshold once the pixel queue is empty, 0 = unchanged (crt_renderer_set_drain_threshold)."""
+        check(_lib.hip().crt_renderer_set_drain_threshold(self.h, int(lanes)), "set_drain_threshold")
+
     def set_xcd_regions(self, on: bool):
         """Variant 8: XCD groups render equal-cost screen strips (crt_renderer_set_xcd_regions)."""
         check(_lib.hip().crt_renderer_set_xcd_regions(self.h, int(bool(on))), "set_xcd_regions")

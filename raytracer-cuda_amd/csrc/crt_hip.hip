@@ -80,6 +80,7 @@ struct RenderParams {
     uint32_t* __restrict__ pix_rays;      // variant 7: rays each pixel took this frame (the next frame's tile order)
     int crit_tiles, crit_threshold;       // variant 8: the first crit_tiles tiles of the cost order regenerate at
                                           // crit_threshold parked lanes instead of regen_threshold
+    int drain_threshold;                  // variant 7: the threshold once the pixel queue is empty
     int top_levels;                       // 4-wide variants: a new ray's first node steps taken from LDS (<= CRT_TOP_LEVELS)
     int carry_lanes, carry_max;           // variant 8 leaf-pair carry (traverse_step4c): a step's part-empty round of
                                           // at most carry_max pairs waits for the next step when at least carry_lanes
@@ -1684,7 +1685,10 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             const int n_parked = __popcll(wave_ballot(parked));
             const int n_live = __popcll(wave_ballot(live));
             const uint64_t c0 = COUNT ? shader_clock() : 0;
-            if (n_parked >= P.regen_threshold || n_parked == n_live) {
+            // once the queue is empty the wave only drains: its last paths no longer wait for many parked lanes
+            // (crt_renderer_set_drain_threshold)
+            const int regen_t = exhausted ? P.drain_threshold : P.regen_threshold;
+            if (n_parked >= regen_t || n_parked == n_live) {
                 if (COUNT) cnt.passes++;
                 if (parked) {
                     if (has_result) finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, c0);
@@ -2941,6 +2945,7 @@ struct crt_renderer {
     int xcd_regions = 0;           // variant 8: XCD groups render screen strips (crt_xcd_order_kernel)
     int probe_stride = 0;          // variant 8's cost probe: every probe_stride-th pixel in x and y (0 = automatic)
     int temporal = 0;              // variant 7: tiles ordered by the previous variant-7 frame's rays per pixel
+    int drain_threshold = 0;       // variant 7: regeneration threshold once the pixel queue is empty (0 = unchanged)
     uint32_t* d_pix_rays = nullptr;   // variant 7 with the temporal order: rays per pixel of the last frame
     uint32_t* d_tile_order = nullptr; // its tiles, most expensive first
     bool pix_rays_valid = false;
@@ -3468,6 +3473,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     dim3 grid((R->width + 15) / 16, (R->height + 15) / 16), block(256);
     const bool cnt = (flags & CRT_RENDER_COUNT_WORK) != 0;
     P.regen_threshold = S->width == 4 ? R->regen_threshold_wide : R->regen_threshold;
+    P.drain_threshold = R->drain_threshold > 0 ? R->drain_threshold : P.regen_threshold;
     if (R->tile_shards > 1) {
         // pixel sharding: variant 8 renders this shard's tiles; every other pixel of the framebuffer is 0, so the sum
         // of the shards' framebuffers (one collective) is the unsharded frame exactly (x + 0 = x).  Checked and
@@ -3800,7 +3806,7 @@ int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene*
     P.n_nodes = A->n_nodes; P.n_mats = A->n_mats; P.n_prims = A->n_prims; P.n_layouts = A->layouts;
     P.err = reinterpret_cast<unsigned*>(R->d_counters + ERR_WORD);
     P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
-    P.accumulate = 0; P.regen_threshold = 64;
+    P.accumulate = 0; P.regen_threshold = 64; P.drain_threshold = 64;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     P.rcp_w = R->rcp_w; P.rcp_h = R->rcp_h; P.fast_uv = R->fast_uv;
     P.probe_stride = 1;
@@ -3968,6 +3974,12 @@ int crt_renderer_set_temporal_order(crt_renderer* R, int on) {
     if (!R || on < 0 || on > 1) return set_error(CRT_ERR_INVALID_ARGUMENT, "temporal order: 0 or 1");
     R->temporal = on;
     R->pix_rays_valid = false;
+    return CRT_OK;
+}
+
+int crt_renderer_set_drain_threshold(crt_renderer* R, int lanes) {
+    if (!R || lanes < 0 || lanes > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "drain threshold 0..64");
+    R->drain_threshold = lanes;
     return CRT_OK;
 }
 

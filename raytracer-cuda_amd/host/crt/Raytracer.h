@@ -39,6 +39,8 @@ struct RaytracerOptions {
     // variant 7 (the < 64-spp frames of the loop) dispatches its tiles most expensive first by the previous frame's rays
     // per pixel (crt_renderer_set_temporal_order): consecutive frames share the cost map; results never depend on it
     bool temporalOrder = true;
+    // variant 7's regeneration threshold once its pixel queue is empty (crt_renderer_set_drain_threshold; 0 = unchanged)
+    int drainThreshold = 0;
 };
 
 struct FrameInfo {
@@ -61,6 +63,7 @@ public:
           m_Renderer(width, height, opts.device) {
         initializeScene();
         CRT_CHECK(crt_renderer_set_temporal_order(m_Renderer.handle(), opts.temporalOrder ? 1 : 0));
+        CRT_CHECK(crt_renderer_set_drain_threshold(m_Renderer.handle(), opts.drainThreshold));
     }
 
     // Raytracer::updateAndRender (Raytracer.h:94-102) for one frame of input.

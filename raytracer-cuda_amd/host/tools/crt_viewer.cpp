@@ -3,7 +3,7 @@
 // frame times are reported (the reference throttles to 60 fps; here frames run back to back).
 //
 //   crt_viewer [-w W] [-h H] [-frames N] [-script still|walk|orbit|hq] [-bvh reference|rebuilt]
-//              [-accumulate] [-no-temporal] [-seed S] [-o last.png] model.obj...
+//              [-accumulate] [-no-temporal] [-drain LANES] [-seed S] [-o last.png] model.obj...
 //
 // Scripts: still = no input (1 spp per frame, RNG continues); walk = W held; orbit = right mouse dragged
 // in a circle; hq = F pressed once, then still (2000 spp frames).
@@ -37,6 +37,7 @@ int main(int argc, char** argv) {
             else if (a == "-o") { need(1); out = argv[++i]; }
             else if (a == "-accumulate") opts.accumulate = true;
             else if (a == "-no-temporal") opts.temporalOrder = false;
+            else if (a == "-drain") { need(1); opts.drainThreshold = std::atoi(argv[++i]); }
             else if (a == "-bvh") {
                 need(1);
                 std::string m = argv[++i];
@@ -85,11 +86,11 @@ int main(int argc, char** argv) {
         const size_t n = s.size();
         auto pct = [&](double p) { return n ? s[std::min(n - 1, (size_t)(p * (n - 1) + 0.5))] : 0.0; };
         std::printf("{\"width\": %d, \"height\": %d, \"script\": \"%s\", \"bvh\": \"%s\", \"accumulate\": %s, "
-                    "\"frames\": %lld, \"fps\": %.1f, \"frame_ms_mean\": %.3f, \"frame_ms_p50\": %.3f, "
+                    "\"temporal\": %s, \"drain\": %d, \"frames\": %lld, \"fps\": %.1f, \"frame_ms_mean\": %.3f, \"frame_ms_p50\": %.3f, "
                     "\"frame_ms_p99\": %.3f, \"kernel_ms_mean\": %.3f, \"samples_per_pixel_total\": %lld, "
                     "\"paths_per_s\": %.4g, \"last_accumulated\": %d}\n",
                     W, H, script.c_str(), opts.scene.bvh == CRT_BVH_REBUILT ? "rebuilt" : "reference",
-                    opts.accumulate ? "true" : "false", frames, n ? 1000.0 * n / tot : 0.0, n ? tot / n : 0.0,
+                    opts.accumulate ? "true" : "false", opts.temporalOrder ? "true" : "false", opts.drainThreshold, frames, n ? 1000.0 * n / tot : 0.0, n ? tot / n : 0.0,
                     pct(0.5), pct(0.99), n ? ktot / n : 0.0, samples,
                     tot > 0 ? (double)W * H * samples / (tot / 1e3) : 0.0, last.accumulated);
         return EXIT_SUCCESS;

@@ -92,16 +92,18 @@ def test_accumulate_equals_one_frame_of_k_spp(scenes, oracle_scenes):
 def test_temporal_order_is_bit_identical(device_scenes):
     """Variant 7 with the temporal tile order (crt_renderer_set_temporal_order): from the second frame on, tiles are
     dispatched by the previous frame's rays per pixel; 1-spp frames accumulated over 4 frames (RNG state continuing) give
-    the same sums, RNG state and ray counts as row order, at a ragged size too."""
+    the same sums, RNG state and ray counts as row order, at a ragged size too.  So do drain thresholds
+    (crt_renderer_set_drain_threshold: 1 and 8 parked lanes once the pixel queue is empty)."""
     import numpy as np
     import crt_amd
     hs, _ = device_scenes["cornell_bunny"]
     sc = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
     for w, h in ((640, 360), (100, 37)):
         out = []
-        for on in (False, True):
+        for on, drain in ((False, 0), (True, 0), (True, 1), (False, 8)):
             r = crt_amd.Renderer(w, h)
             r.set_temporal_order(on)
+            r.set_drain_threshold(drain)
             r.set_camera(crt_amd.camera(1))
             r.init_rand(41)
             rays = []
@@ -111,4 +113,5 @@ def test_temporal_order_is_bit_identical(device_scenes):
                 assert r.last_kernel_name().startswith("crt_render_kernel<false, 7,")
                 rays.append(r.counters()["rays"])
             out.append((r.linear().view(np.uint32), r.rng_state(), rays))
-        assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1]) and out[0][2] == out[1][2]
+        for o in out[1:]:
+            assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1]) and out[0][2] == o[2]
