@@ -65,7 +65,8 @@ class HostScene:
         return float(_lib.host().crth_scene_build_ms(self.h))
 
     def __del__(self):
-        if getattr(self, "h", None):
+        # at interpreter exit the module's globals may already be gone (None); the process frees the scene then
+        if getattr(self, "h", None) and _lib is not None:
             _lib.host().crth_scene_destroy(self.h)
             self.h = None
 
@@ -181,7 +182,7 @@ class Scene:
         return {k: getattr(s, k) for k, _ in SceneStats._fields_}
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and _lib is not None:   # None: interpreter exit (see HostScene.__del__)
             _lib.hip().crt_scene_destroy(self.h)
             self.h = None
 
@@ -210,7 +211,7 @@ class Renderer:
         return r
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and _lib is not None:   # None: interpreter exit (see HostScene.__del__)
             if getattr(self, "_owned", True):
                 _lib.hip().crt_renderer_destroy(self.h)
             self.h = None
@@ -403,7 +404,7 @@ class CameraController:
         self.h = h
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and _lib is not None:   # None: interpreter exit (see HostScene.__del__)
             _lib.host().crth_camera_destroy(self.h)
             self.h = None
 
@@ -438,7 +439,7 @@ class Viewer:
         self.renderer = Renderer._borrow(_lib.host().crth_viewer_renderer(h), width, height, device, self)
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and _lib is not None:   # None: interpreter exit (see HostScene.__del__)
             self.renderer.h = None
             _lib.host().crth_viewer_destroy(self.h)
             self.h = None
