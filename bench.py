@@ -108,6 +108,8 @@ def parse():
     ap.add_argument("--critical-tiles", type=int, default=None,
                     help="variant 8: leading tiles of the cost order that regenerate sooner (default: library's)")
     ap.add_argument("--critical-lanes", type=int, default=16, help="their regeneration threshold")
+    ap.add_argument("--wave-drain", type=int, default=None,
+                    help="variants 4/8: a draining wave passes at this many 64ths of its live lanes (64 = all)")
     ap.add_argument("--drain-threshold", type=int, default=None,
                     help="variant 7: regeneration threshold once the pixel queue is empty (0 = unchanged)")
     ap.add_argument("--carry", type=int, nargs=2, default=None, metavar=("LANES", "MAX_PAIRS"),
@@ -379,6 +381,8 @@ def main():
         r.set_xcd_regions(args.xcd_regions)
     if args.drain_threshold is not None:
         r.set_drain_threshold(args.drain_threshold)
+    if args.wave_drain is not None:
+        r.set_wave_drain(args.wave_drain)
     r.set_camera(cam)
     fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard,
                               collective=grouped)

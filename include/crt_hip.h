@@ -282,6 +282,10 @@ int  crt_renderer_set_temporal_order(crt_renderer* r, int on);
  * at `lanes` parked lanes (1..64) instead of the regeneration threshold, so they wait less for each other; 0 = the
  * regeneration threshold (the default).  Results never depend on it. */
 int  crt_renderer_set_drain_threshold(crt_renderer* r, int lanes);
+/* Variants 4 and 8: once fewer than the regeneration threshold of a wave's lanes still have samples, a shading pass
+ * runs when `sixty_fourths`/64 of those live lanes are parked (1..64; 64 = only when all of them are; default 48), so
+ * the wave's last pixels wait less for each other's paths.  Results never depend on it. */
+int  crt_renderer_set_wave_drain(crt_renderer* r, int sixty_fourths);
 /* Variant 8 with the cost probe: 1 = the blocks that share an XCD (block index mod 8, MI355X's round-robin dispatch)
  * render one screen strip of equal probe cost, most expensive tile first, so each XCD's L2 holds its strip's geometry;
  * 0 = one global cost order (default).  Ignored with pixel sharding.  Results never depend on it. */

@@ -318,6 +318,10 @@ class Renderer:
         """Variant 7: regeneration threshold once the pixel queue is empty, 0 = unchanged (crt_renderer_set_drain_threshold)."""
         check(_lib.hip().crt_renderer_set_drain_threshold(self.h, int(lanes)), "set_drain_threshold")
 
+    def set_wave_drain(self, sixty_fourths: int):
+        """Variants 4/8: a draining wave passes at sixty_fourths/64 of its live lanes (crt_renderer_set_wave_drain)."""
+        check(_lib.hip().crt_renderer_set_wave_drain(self.h, int(sixty_fourths)), "set_wave_drain")
+
     def set_xcd_regions(self, on: bool):
         """Variant 8: XCD groups render equal-cost screen strips (crt_renderer_set_xcd_regions)."""
         check(_lib.hip().crt_renderer_set_xcd_regions(self.h, int(bool(on))), "set_xcd_regions")

@@ -81,6 +81,7 @@ struct RenderParams {
     int crit_tiles, crit_threshold;       // variant 8: the first crit_tiles tiles of the cost order regenerate at
                                           // crit_threshold parked lanes instead of regen_threshold
     int drain_threshold;                  // variant 7: the threshold once the pixel queue is empty
+    int wave_drain;                       // variants 4/8: sixty-fourths of the live lanes a draining wave passes at
     int top_levels;                       // 4-wide variants: a new ray's first node steps taken from LDS (<= CRT_TOP_LEVELS)
     int carry_lanes, carry_max;           // variant 8 leaf-pair carry (traverse_step4c): a step's part-empty round of
                                           // at most carry_max pairs waits for the next step when at least carry_lanes
@@ -1796,7 +1797,11 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             const int n_live = __popcll(live_mask);
             if (n_live == 0) break;
             const uint64_t c0 = COUNT ? shader_clock() : 0;
-            if (n_parked >= regen_t || n_parked == n_live) {
+            // once fewer than regen_t lanes still have samples, waiting for every live lane to park before a pass makes
+            // each of them wait for the slowest path of the others at every bounce; a pass at wave_drain/64 of them
+            // (crt_renderer_set_wave_drain; 64 = all) shortens the wave's own drain (profiles/r04n)
+            const bool drain_pass = n_live < regen_t && n_parked * 64 >= n_live * P.wave_drain;
+            if (n_parked >= regen_t || n_parked == n_live || drain_pass) {
                 if (COUNT) cnt.passes++;
                 if (__builtin_amdgcn_inverse_ballot_w64(parked_mask)) {
                     const uint64_t s0 = COUNT ? shader_clock() : 0;
@@ -2946,6 +2951,7 @@ struct crt_renderer {
     int probe_stride = 0;          // variant 8's cost probe: every probe_stride-th pixel in x and y (0 = automatic)
     int temporal = 0;              // variant 7: tiles ordered by the previous variant-7 frame's rays per pixel
     int drain_threshold = 0;       // variant 7: regeneration threshold once the pixel queue is empty (0 = unchanged)
+    int wave_drain = 48;           // variants 4/8: draining waves pass at 48/64 of their live lanes (profiles/r04n)
     uint32_t* d_pix_rays = nullptr;   // variant 7 with the temporal order: rays per pixel of the last frame
     uint32_t* d_tile_order = nullptr; // its tiles, most expensive first
     bool pix_rays_valid = false;
@@ -3474,6 +3480,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     const bool cnt = (flags & CRT_RENDER_COUNT_WORK) != 0;
     P.regen_threshold = S->width == 4 ? R->regen_threshold_wide : R->regen_threshold;
     P.drain_threshold = R->drain_threshold > 0 ? R->drain_threshold : P.regen_threshold;
+    P.wave_drain = R->wave_drain;
     if (R->tile_shards > 1) {
         // pixel sharding: variant 8 renders this shard's tiles; every other pixel of the framebuffer is 0, so the sum
         // of the shards' framebuffers (one collective) is the unsharded frame exactly (x + 0 = x).  Checked and
@@ -3806,7 +3813,7 @@ int crt_scene_compare_dump(crt_renderer* R, const crt_scene* A, const crt_scene*
     P.n_nodes = A->n_nodes; P.n_mats = A->n_mats; P.n_prims = A->n_prims; P.n_layouts = A->layouts;
     P.err = reinterpret_cast<unsigned*>(R->d_counters + ERR_WORD);
     P.width = R->width; P.height = R->height; P.spp = spp; P.max_bounces = max_bounces;
-    P.accumulate = 0; P.regen_threshold = 64; P.drain_threshold = 64;
+    P.accumulate = 0; P.regen_threshold = 64; P.drain_threshold = 64; P.wave_drain = 64;
     P.rng = R->d_rng; P.sum = R->d_sum; P.counters = R->d_counters; P.cam = R->cam;
     P.rcp_w = R->rcp_w; P.rcp_h = R->rcp_h; P.fast_uv = R->fast_uv;
     P.probe_stride = 1;
@@ -3980,6 +3987,12 @@ int crt_renderer_set_temporal_order(crt_renderer* R, int on) {
 int crt_renderer_set_drain_threshold(crt_renderer* R, int lanes) {
     if (!R || lanes < 0 || lanes > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "drain threshold 0..64");
     R->drain_threshold = lanes;
+    return CRT_OK;
+}
+
+int crt_renderer_set_wave_drain(crt_renderer* R, int sixty_fourths) {
+    if (!R || sixty_fourths < 1 || sixty_fourths > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "wave drain 1..64");
+    R->wave_drain = sixty_fourths;
     return CRT_OK;
 }
 

@@ -366,3 +366,24 @@ def test_probe_stride_is_bit_identical(rebuilt, stride):
             assert r.last_timings()["probe_sort_ms"] > 0
             out.append((r.linear().view(np.uint32), r.rng_state(), r.counters()["rays"]))
         assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1]) and out[0][2] == out[1][2]
+
+
+def test_wave_drain_is_bit_identical(rebuilt):
+    """Variants 8 and 4 with draining waves passing at 16/64 and 48/64 (the default) of their live lanes instead of all
+    of them (crt_renderer_set_wave_drain): only when lanes run their shading passes changes, so frames, RNG state and ray
+    counts equal those of 64/64, at a ragged size too."""
+    dev = rebuilt["cornell_bunny", "w4"]
+    for w, h, spp, variant in ((640, 360, 64, 8), (100, 37, 70, 8), (160, 90, 8, 4)):
+        out = []
+        for wd in (64, 48, 16):
+            r = crt_amd.Renderer(w, h)
+            r.set_kernel_variant(variant)
+            r.set_wave_drain(wd)
+            r.set_camera(crt_amd.camera(spp))
+            r.init_rand(41)
+            r.render(dev, spp, 20)
+            r.synchronize()
+            assert r.last_kernel_name().startswith(f"crt_render_kernel<false, {variant},")
+            out.append((r.linear().view(np.uint32), r.rng_state(), r.counters()["rays"]))
+        for o in out[1:]:
+            assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1]) and out[0][2] == o[2]

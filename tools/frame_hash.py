@@ -22,6 +22,7 @@ ap.add_argument("--occupancy", type=int, default=0, help="crt_renderer_set_occup
 ap.add_argument("--xcd-regions", type=int, default=0, help="crt_renderer_set_xcd_regions (variant 8 tile order)")
 ap.add_argument("--probe-stride", type=int, default=0, help="variant 8's probe stride (crt_renderer_set_schedule; 0 = auto)")
 ap.add_argument("--drain", type=int, default=0, help="variant 7's drain threshold (crt_renderer_set_drain_threshold)")
+ap.add_argument("--wave-drain", type=int, default=0, help="variants 4/8 wave drain in 64ths (crt_renderer_set_wave_drain)")
 a = ap.parse_args()
 
 hs = crt_amd.HostScene(assets.scene_files("cornell_bunny"), build_device=0)
@@ -43,6 +44,8 @@ for sc_name, w, h, spp, var, count in cases:
         r.set_schedule(-1, 64, probe_stride=a.probe_stride)
     if a.drain:
         r.set_drain_threshold(a.drain)
+    if a.wave_drain:
+        r.set_wave_drain(a.wave_drain)
     r.set_camera(crt_amd.camera(spp))
     r.init_rand(41)
     r.render(wide if sc_name == "w4" else ref, spp, 20, count_work=count)
