@@ -31,6 +31,7 @@ ap.add_argument("--temporal", action="store_true",
                 help="variant 7: render a first frame, then time the second with its tiles ordered by the first's "
                      "rays per pixel (crt_renderer_set_temporal_order)")
 ap.add_argument("--drain", type=int, default=0, help="variant 7's drain threshold (crt_renderer_set_drain_threshold)")
+ap.add_argument("--wave-drain", type=int, default=48, help="variants 4/8 wave drain in 64ths (crt_renderer_set_wave_drain)")
 a = ap.parse_args()
 
 hs = crt_amd.HostScene(assets.scene_files(a.scene))
@@ -38,6 +39,7 @@ sc = hs.upload(0, bvh=a.bvh, width=4, leaf_size=4, traversal_cost=2.0) if a.bvh 
 r = crt_amd.Renderer(a.w, a.h)
 r.set_kernel_variant(a.variant)
 r.set_drain_threshold(a.drain)
+r.set_wave_drain(a.wave_drain)
 r.set_camera(crt_amd.camera(a.spp))
 r.init_rand(41)
 if a.temporal:
@@ -73,7 +75,7 @@ for i in range(20):
     lo, hi = bins[i], bins[i + 1]
     ov = np.clip(np.minimum(end, hi) - np.maximum(start, lo), 0, None).sum() / (hi - lo)
     occ.append(round(float(ov), 1))
-out = {"scene": a.scene, "bvh": a.bvh, "variant": a.variant, "temporal": a.temporal, "drain": a.drain, "kernel": r.last_kernel_name(), "spp": a.spp, "kernel_ms": round(kernel_ms, 3), "span_ms": round(span / 1e3, 3),
+out = {"scene": a.scene, "bvh": a.bvh, "variant": a.variant, "temporal": a.temporal, "drain": a.drain, "wave_drain": a.wave_drain, "kernel": r.last_kernel_name(), "spp": a.spp, "kernel_ms": round(kernel_ms, 3), "span_ms": round(span / 1e3, 3),
        "waves": n_waves, "peak_resident_waves": peak, "occupancy_efficiency": round(eff, 4),
        "tail_ms": round((span - steady_end) / 1e3, 3), "tail_fraction": round((span - steady_end) / span, 4),
        "wave_ms": {"min": round(float(dur.min()) / 1e3, 3), "median": round(float(np.median(dur)) / 1e3, 3),
