@@ -1,19 +1,14 @@
 #!/bin/bash
 # The current one-off GPU job (overwritten per job; the copy that ran is kept as profiles/<id>/job.sh).
-# r04w: verification at the round-4 HEAD as the driver runs it: the GPU suite, smoke, the default bench, and the RCCL
-# one-rank bench.
+# r04x: the wave drain's fraction and the regeneration threshold around their defaults on config C itself (2000 spp),
+# interleaved, for the next round's plan; no change to the tree.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=r04w; OUT=$R/gpurun_out/$O; mkdir -p $OUT
+O=r04x; OUT=$R/gpurun_out/$O; mkdir -p $OUT
 cd $R
-sha256sum raytracer-cuda_amd/csrc/crt_hip.hip raytracer-cuda_amd/lib/libcrt_hip.so bench.py > $OUT/sha.txt
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
-tail -1 $OUT/pytest_gpu.log
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
-tail -2 $OUT/smoke.log
-timeout -k 10 400 python3 bench.py > $OUT/bench.log 2>&1
-tail -1 $OUT/bench.log | cut -c1-200
-timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
-    --master-port 29516 bench.py --gpus 1 --steps 3 --warmup 1 > $OUT/bench_rccl1.log 2>&1
-tail -1 $OUT/bench_rccl1.log | cut -c1-200
+sha256sum raytracer-cuda_amd/csrc/crt_hip.hip raytracer-cuda_amd/lib/libcrt_hip.so > $OUT/sha.txt
+timeout -k 10 400 python3 tools/schedule_sweep.py --world 1 --reps 4 --set wd48: wd40:wd=40 wd56:wd=56 wd32:wd=32 wd64:wd=64 T42:T=42 T46:T=46 > $OUT/sweep_C.jsonl
+python3 -c "
+import json
+for d in map(json.loads, open('$OUT/sweep_C.jsonl')): print(d['name'], d['main_median_ms'], d['main_ms_reps'])"
 echo job done
