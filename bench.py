@@ -62,7 +62,14 @@ HBM_PEAK_GBS = 8000.0            # MI355X HBM3E, MI355X_MICROARCH.md chip table 
 # Algorithmic bytes / FP ops per unit of work:
 B_BOX, B_TRI, B_SPHERE, B_RAY = 32, 36, 20, 16     # node box+link; v0,e1,e2; c,r,r^2; material/hit
 B_PIXEL = 24 + 24 + 12                              # RNG state in + out, fp32 sum out
+# f32 operations per unit, counted function by function in the reference source ("Algorithmic operation
+# counts"): AABB::hit without its per-visit reciprocals (hoisted per ray) and without the throw-away hit record; the
+# whole Moller-Trumbore test without the two edge subtractions (precomputed, bit-identical); Sphere::hit to its first
+# root; per ray the camera ray (amortised), the hit record, the material scatter and Russian roulette
 F_BOX, F_TRI, F_SPHERE, F_RAY = 24, 54, 30, 100
+# SURVEY §8(d)'s own weights, F_ray = 23*N_node + 33*N_tri + ~40 (MT with its early exits at the average reject point;
+# no sphere term), reported beside the builder's
+F_SURVEY_BOX, F_SURVEY_TRI, F_SURVEY_RAY = 23, 33, 40
 
 
 def log(*a):
@@ -112,8 +119,9 @@ def parse():
                     help="variants 4/8: a draining wave passes at this many 64ths of its live lanes (64 = all)")
     ap.add_argument("--drain-threshold", type=int, default=None,
                     help="variant 7: regeneration threshold once the pixel queue is empty (0 = unchanged)")
-    ap.add_argument("--carry", type=int, nargs=2, default=None, metavar=("LANES", "MAX_PAIRS"),
-                    help="variant 8 leaf-pair carry (crt_renderer_set_leaf_carry; CRT_LEAF_CARRY builds)")
+    ap.add_argument("--tail-lanes", type=int, default=None,
+                    help="variant 8: a wave whose live lanes drop to this many finishes them in the per-lane tail loop "
+                         "(crt_renderer_set_tail_mode; 0 = off; default: the library's)")
     ap.add_argument("--xcd-regions", type=int, default=None, choices=[0, 1],
                     help="variant 8: XCD groups render equal-cost screen strips (crt_renderer_set_xcd_regions)")
     ap.add_argument("--bvh", default="rebuilt", choices=["rebuilt", "reference"])
@@ -242,7 +250,8 @@ def roofline_counters(key: str, kname: str):
     return e if e and e.get("kernel") == kname else None
 
 
-def roofline_from_counters(e, rays: int, kernel_s: float, algorithmic_ops: int | None = None):
+def roofline_from_counters(e, rays: int, kernel_s: float, algorithmic_ops: int | None = None,
+                           survey_ops: int | None = None):
     """Utilisation of the units that can bind the render kernel, from the per-ray counter values of the committed
     PMC run (same workload, same kernel) scaled by THIS run's exact ray count and HIP-event kernel time.  The bound is
     the unit with the largest fraction of its peak (MI355X_MICROARCH.md chip table: 1024 SIMDs at 2.4 GHz, a wave64
@@ -264,6 +273,13 @@ def roofline_from_counters(e, rays: int, kernel_s: float, algorithmic_ops: int |
                                 "unit": "TOP/s (SURVEY §8(d) f32 ops: 24*box + 54*tri + 30*sphere + 100*ray)",
                                 "frac": round(alg / valu_peak, 4),
                                 "issued_over_algorithmic": round(valu / alg, 3)}
+    if survey_ops:
+        alg = survey_ops / kernel_s / 1e12
+        units["algorithmic_survey"] = {"achieved": round(alg, 3), "peak": round(valu_peak, 2),
+                                       "unit": "TOP/s (SURVEY §8(d)'s weights: 23*box + 33*tri + 40*ray)",
+                                       "frac": round(alg / valu_peak, 4),
+                                       "frac_of_fma_doubled_peak": round(alg / (2 * valu_peak), 4),
+                                       "issued_over_algorithmic": round(valu / alg, 3)}
     if "TCP_TOTAL_CACHE_ACCESSES" in pr and "vl1_calibration" in e:
         acc = pr["TCP_TOTAL_CACHE_ACCESSES"] * rays / kernel_s / 1e12
         cal = e["vl1_calibration"]
@@ -276,7 +292,7 @@ def roofline_from_counters(e, rays: int, kernel_s: float, algorithmic_ops: int |
     if "hbm_bytes_per_launch" in d:
         hbm = d["hbm_bytes_per_launch"] / e["rays_per_launch"] * rays / kernel_s / 1e9
         units["hbm"] = {"achieved": round(hbm, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(hbm / HBM_PEAK_GBS, 5)}
-    bound = max((k for k in units if k != "algorithmic"), key=lambda k: units[k]["frac"])
+    bound = max((k for k in units if not k.startswith("algorithmic")), key=lambda k: units[k]["frac"])
     u = units[bound]
     traffic = (d["hbm_bytes_per_launch"] / e["rays_per_launch"] * rays) if "hbm_bytes_per_launch" in d else None
     return {"bound": bound, "achieved": u["achieved"], "peak": u["peak"], "unit": u["unit"], "frac": u["frac"],
@@ -298,7 +314,7 @@ def main():
 
     import crt_amd
     from crt_amd import assets
-    from crt_amd.dist import ShardedFrameRenderer, dist_env
+    from crt_amd.dist import ShardedFrameRenderer, dist_env, gather_frame_timings
 
     rank, local, world = dist_env()
     if world != args.gpus:
@@ -364,26 +380,31 @@ def main():
           f"{st['device_bytes'] / 1e6:.1f} MB in HBM, load+build+upload {t_scene:.2f}s {setup}")
 
     cam = crt_amd.camera(args.spp)
-    r = crt_amd.Renderer(W, H, local)
-    if args.kernel_variant is not None:
-        r.set_kernel_variant(args.kernel_variant)
-    if args.regen_threshold is not None:
-        r.set_regen_threshold(args.regen_threshold)
-    if args.occupancy is not None:
-        r.set_occupancy_target(args.occupancy)
-    if args.probe_spp is not None or args.probe_stride:
-        r.set_schedule(-1 if args.probe_spp is None else args.probe_spp, 64, probe_stride=args.probe_stride)
-    if args.critical_tiles is not None:
-        r.set_critical_tiles(args.critical_tiles, args.critical_lanes)
-    if args.carry is not None:
-        r.set_leaf_carry(*args.carry)
-    if args.xcd_regions is not None:
-        r.set_xcd_regions(args.xcd_regions)
-    if args.drain_threshold is not None:
-        r.set_drain_threshold(args.drain_threshold)
-    if args.wave_drain is not None:
-        r.set_wave_drain(args.wave_drain)
-    r.set_camera(cam)
+
+    def make_renderer():
+        rr = crt_amd.Renderer(W, H, local)
+        if args.kernel_variant is not None:
+            rr.set_kernel_variant(args.kernel_variant)
+        if args.regen_threshold is not None:
+            rr.set_regen_threshold(args.regen_threshold)
+        if args.occupancy is not None:
+            rr.set_occupancy_target(args.occupancy)
+        if args.probe_spp is not None or args.probe_stride:
+            rr.set_schedule(-1 if args.probe_spp is None else args.probe_spp, 64, probe_stride=args.probe_stride)
+        if args.critical_tiles is not None:
+            rr.set_critical_tiles(args.critical_tiles, args.critical_lanes)
+        if args.xcd_regions is not None:
+            rr.set_xcd_regions(args.xcd_regions)
+        if args.drain_threshold is not None:
+            rr.set_drain_threshold(args.drain_threshold)
+        if args.wave_drain is not None:
+            rr.set_wave_drain(args.wave_drain)
+        if args.tail_lanes is not None:
+            rr.set_tail_mode(args.tail_lanes)
+        rr.set_camera(cam)
+        return rr
+
+    r = make_renderer()
     fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard,
                               collective=grouped)
     log_r(f"[plan] {world} rank(s), spp per rank {[fr.spp] if world == 1 else 'spp/N'}")
@@ -394,29 +415,66 @@ def main():
         torch.cuda.synchronize()
         log_r(f"[warmup {i}] {time.perf_counter() - t:.3f}s")
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    fr.reset_timings()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        fr.render(*evs[k])
+        fr.render()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     elapsed = allreduce_max(elapsed)
-    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    # per frame: this rank's render (RNG reset excluded; probe, sort and main kernel) and its collective, HIP events on
+    # the launch stream; gathered over ranks (a collective: every rank calls it)
+    frame_t = fr.frame_timings()
+    kernel_ms = [f[0] for f in frame_t]
     kernel_ms_avg = sum(kernel_ms) / len(kernel_ms)
     kernel_ms_max = allreduce_max(max(kernel_ms))
+    dist_t = gather_frame_timings(fr) if grouped else None
     rays_rank = r.counters()["rays"]
     kname = r.last_kernel_name()      # the instantiation the timed frames ran (rocprofv3's spelling)
     phases = r.last_timings()         # the last timed frame: probe + tile sort, and the main render kernel alone
     # every timed frame's phases (the renderer keeps the last 32 frames' HIP events): the roofline divides by the
-    # main kernel's average over the timed frames, the same quantity rocprofv3's average duration measures
-    hist = [r.timing_history(k) for k in range(min(args.steps, 32))]
+    # main kernel's average over the timed frames, the same quantity rocprofv3's average duration measures.  A base
+    # library from before ABI 3 (tools/gpu_job.sh A/B runs) has no history: the last frame's phases stand in.
+    if r.has_timing_history():
+        hist = [r.timing_history(k) for k in range(min(args.steps, 32))]
+    else:
+        hist = [phases]
     phases_avg = {k: sum(h[k] for h in hist) / len(hist) for k in hist[0]}
     [rays_frame] = allreduce_sum_i([rays_rank])
     log_r(f"[timed] {args.steps} frames in {elapsed:.3f}s; render kernel {kernel_ms_avg:.1f} ms avg (rank 0); "
-          f"{rays_frame} rays/frame")
+          f"{rays_frame} rays/frame" + (f"; {dist_t}" if dist_t else ""))
+
+    # end to end (RNG init + BVH upload + render + reduce + readback, CUDARenderer.cuh:39-60 and
+    # WindowManager.h:87): the scene's load + BVH builds + upload measured above, plus a fresh renderer (its own
+    # curand_init, no cached state), one frame with the collective and the resolve, and the RGBA8 D2H readback on
+    # rank 0, max over ranks
+    barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    r_e2e = make_renderer()
+    fr_e2e = ShardedFrameRenderer(r_e2e, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard,
+                                  collective=grouped)
+    fr_e2e.render()
+    if rank == 0:
+        r_e2e.rgba8()
+    torch.cuda.synchronize()
+    t_frame_e2e = allreduce_max(time.perf_counter() - t)
+    t_rb = time.perf_counter()
+    if rank == 0:
+        r_e2e.rgba8()
+    t_readback = time.perf_counter() - t_rb
+    del fr_e2e, r_e2e
+    end_to_end = {"end_to_end_s": round(t_scene + t_frame_e2e, 4),
+                  "scene_load_build_upload_s": round(t_scene, 4),
+                  "fresh_renderer_frame_readback_s": round(t_frame_e2e, 4),
+                  "rgba8_readback_ms": round(t_readback * 1e3, 3),
+                  "note": "scene: OBJ load + mesh BVH build + rebuilt-tree build + upload; then a new renderer "
+                          "(curand_init by the jump kernel, not the cache) + one frame + collective + resolve + "
+                          "RGBA8 D2H to host (rank 0); max over ranks"}
+    log_r(f"[e2e] {end_to_end}")
 
     if args.save_ppm and rank == 0:
         img = r.rgba8()
@@ -444,11 +502,14 @@ def main():
                         + B_RAY * work["rays"] + B_PIXEL * W * H)
         flops_launch = (F_BOX * work["box_tests"] + F_TRI * work["tri_tests"] + F_SPHERE * work["sphere_tests"]
                         + F_RAY * work["rays"])
+        survey_launch = F_SURVEY_BOX * work["box_tests"] + F_SURVEY_TRI * work["tri_tests"] + F_SURVEY_RAY * work["rays"]
         main_s = phases_avg["main_kernel_ms"] / 1e3
         algorithmic = {"bytes_per_launch": int(bytes_launch),
                        "cache_served_GB_s": round(bytes_launch / main_s / 1e9, 1),
                        "ops_per_launch": int(flops_launch),
                        "ops_TOP_s": round(flops_launch / main_s / 1e12, 3),
+                       "survey_ops_per_launch": int(survey_launch),
+                       "survey_ops_TOP_s": round(survey_launch / main_s / 1e12, 3),
                        "denominator": "main render kernel's HIP-event time, average over the timed frames (the "
                                       "roofline's)",
                        "per_ray": {"box_tests": round(work["box_tests"] / work["rays"], 3),
@@ -462,7 +523,8 @@ def main():
         # the counters are the main render kernel's alone, so they are divided by its own time (HIP events around that
         # launch only), not by the whole render's, which includes the cost probe and the tile sort
         roofline = roofline_from_counters(ec, rays_rank, phases_avg["main_kernel_ms"] / 1e3,
-                                          algorithmic["ops_per_launch"] if algorithmic else None)
+                                          algorithmic["ops_per_launch"] if algorithmic else None,
+                                          algorithmic["survey_ops_per_launch"] if algorithmic else None)
         roofline.update(kernel=kname, kernel_ms=round(phases_avg["main_kernel_ms"], 3),
                         kernel_ms_note=f"HIP events around the main render launch, average of the {len(hist)} timed "
                                        "frames (probe and tile sort excluded)")
@@ -525,8 +587,12 @@ def main():
             "render_phases_ms_last_frame": {k: round(v, 3) for k, v in phases.items()},
             "render_phases_ms_avg": {k: round(v, 3) for k, v in phases_avg.items()},
             "roofline": roofline, "algorithmic": algorithmic, "cpu_baseline": cpu, "parity": parity,
-            "setup": setup,
+            "setup": setup, "end_to_end": end_to_end, "end_to_end_s": end_to_end["end_to_end_s"],
         }
+        if dist_t is not None:
+            # N > 1 (or a one-rank process group): each rank's render and the time its stream spent in the collective
+            out.update(render_ms_per_rank=dist_t["render_ms_per_rank"], reduce_ms=dist_t["reduce_ms"],
+                       reduce_ms_per_rank=dist_t["reduce_ms_per_rank"], dist_timings=dist_t)
         print(json.dumps(out), flush=True)
     if grouped:
         dist.destroy_process_group()

@@ -269,9 +269,8 @@ int  crt_renderer_set_critical_tiles(crt_renderer* r, int tiles, int lanes);
  * order and the stack entries are the traversal's own, so results never depend on it (a ray whose step hits a leaf
  * child takes that node through the regular step). */
 int  crt_renderer_set_top_levels(crt_renderer* r, int levels);
-/* Variant 8's leaf-pair carry (kernels built with CRT_LEAF_CARRY): a traversal step runs whole rounds of 64 leaf pairs
- * and carries a part-empty remainder of at most `max_pairs` (0..63; 0 = never) pairs to the next step when at least
- * `lanes` (0..64; 65 = never) lanes are still traversing.  Results never depend on it. */
+/* Variant 8's leaf-pair carry, a round-4 experiment that was measured and removed (DESIGN.md §8,
+ * profiles/r04c/leaf_carry.patch).  Kept for ABI stability: returns CRT_ERR_UNSUPPORTED. */
 int  crt_renderer_set_leaf_carry(crt_renderer* r, int lanes, int max_pairs);
 /* Variant 7 without the cost probe (the interactive loop's 1-spp frames): 1 = dispatch its 8x8 tiles most expensive
  * first by the rays per pixel the previous variant-7 render of this renderer counted (consecutive frames share the cost

@@ -327,8 +327,14 @@ class Renderer:
         check(_lib.hip().crt_renderer_set_xcd_regions(self.h, int(bool(on))), "set_xcd_regions")
 
     def set_leaf_carry(self, lanes: int, max_pairs: int):
-        """Variant 8's leaf-pair carry (CRT_LEAF_CARRY builds; crt_renderer_set_leaf_carry)."""
+        """Variant 8's leaf-pair carry: measured and removed in round 5; the library reports
+        CRT_ERR_UNSUPPORTED, so this raises CrtError (profiles/r04c/leaf_carry.patch restores the kernels)."""
         check(_lib.hip().crt_renderer_set_leaf_carry(self.h, int(lanes), int(max_pairs)), "set_leaf_carry")
+
+    @staticmethod
+    def has_timing_history() -> bool:
+        """Whether the loaded library exports crt_renderer_timing_history (ABI >= 3; older base builds in A/B runs)."""
+        return hasattr(_lib.hip(), "crt_renderer_timing_history")
 
     def timing_history(self, back: int) -> dict:
         """last_timings() of an earlier render: back = 0 is the last one, up to 31 (crt_renderer_timing_history)."""

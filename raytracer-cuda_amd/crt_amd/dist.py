@@ -67,13 +67,20 @@ class ShardedFrameRenderer:
         self.seed = int(seed)
         self.rank, self.world, self.group = rank, world, group
         self.reduce_op = reduce_op
-        # the collective runs for every world > 1 and, when asked (or a process group exists), for one rank too: the
-        # production RCCL path on a one-rank communicator (bench.py under torch.distributed.run --nproc-per-node 1)
+        # the collective runs for every world > 1 and, when asked (or when the process group IS this frame's world), for
+        # one rank too: the production RCCL path on a one-rank communicator (bench.py under torch.distributed.run
+        # --nproc-per-node 1).  An unsharded frame (world 1) rendered inside a larger job stays local: summing it over
+        # the default group would add the other ranks' unrelated frames (or hang if they do not call it).
+        import torch.distributed as dist
+        grp_size = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else None
         if collective is None:
-            import torch.distributed as dist
-            collective = world > 1 or (dist.is_available() and dist.is_initialized())
+            collective = world > 1 or grp_size == world
         if world > 1 and not collective:
             raise ValueError("world > 1 needs the framebuffer collective")
+        if collective and grp_size is not None and grp_size != world:
+            raise ValueError(f"the process group has {grp_size} ranks but the frame is sharded over world={world}")
+        if collective and grp_size is None:
+            raise ValueError("the framebuffer collective needs an initialised torch.distributed process group")
         self.collective = bool(collective)
         if mode == "spp":
             self.spp = shard_spp(spp_total, world, rank)
@@ -87,34 +94,96 @@ class ShardedFrameRenderer:
         renderer.attach_linear(self.fb.data_ptr())
         from . import pixel_sample_scale
         self.scale = pixel_sample_scale(self.spp_total)
+        self._marks = []
 
     def stream_handle(self):
         if not str(self.fb_device).startswith("cuda"):
             return None
         return self.torch.cuda.current_stream().cuda_stream
 
+    def _mark(self):
+        """A time mark on the launch stream: a HIP event (GPU framebuffer) or the host clock (CPU, synchronous)."""
+        if str(self.fb_device).startswith("cuda"):
+            ev = self.torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        import time
+        return time.perf_counter()
+
+    @staticmethod
+    def _ms(a, b) -> float:
+        return a.elapsed_time(b) if hasattr(a, "elapsed_time") else (b - a) * 1e3
+
     def render(self, ev_start=None, ev_end=None):
-        """Fresh RNG + this rank's samples + framebuffer reduce + resolve (rank 0 / all)."""
+        """Fresh RNG + this rank's samples + framebuffer reduce + resolve (rank 0 / all).
+
+        Every frame leaves three marks on the launch stream (render start, render end = collective start, collective
+        end), read by frame_timings() after the caller's synchronize: the rank's own render time and the time its
+        stream spent in the collective (which includes waiting for the slowest rank)."""
         st = self.stream_handle()
         self.r.init_rand(self.seed, self.subseq, stream=st)
         if ev_start is not None:
             ev_start.record()
+        m0 = self._mark()
         self.r.render(self.scene, self.spp, self.max_bounces, stream=st)
         if ev_end is not None:
             ev_end.record()
+        m1 = self._mark()
         if self.collective:
             import torch.distributed as dist
             if self.reduce_op == "all_reduce":
                 dist.all_reduce(self.fb, op=dist.ReduceOp.SUM, group=self.group)
             else:
                 dist.reduce(self.fb, dst=0, op=dist.ReduceOp.SUM, group=self.group)
+        m2 = self._mark()
+        self._marks.append((m0, m1, m2))
+        del self._marks[:-64]
         if self.rank == 0 or self.reduce_op == "all_reduce":
             self.r.resolve(self.scale, stream=st)
+
+    def reset_timings(self):
+        self._marks = []
+
+    def frame_timings(self, last: int | None = None):
+        """[(render_ms, reduce_ms)] of the last `last` frames (all kept frames by default); synchronises first."""
+        if str(self.fb_device).startswith("cuda"):
+            self.torch.cuda.synchronize(self.r.device)
+        marks = self._marks if last is None else self._marks[-last:]
+        return [(self._ms(a, b), self._ms(b, c)) for a, b, c in marks]
 
     def linear(self) -> np.ndarray:
         if str(self.fb_device).startswith("cuda"):
             self.torch.cuda.synchronize(self.r.device)
         return self.fb.cpu().numpy()
+
+
+def gather_frame_timings(fr: ShardedFrameRenderer, last: int | None = None, group=None) -> dict:
+    """Per-rank averages of the last frames' render and collective times, gathered to every rank.
+
+    A collective of its own (all_gather of two floats per rank), so every rank of the frame's group must call it.  With
+    no process group (world 1, no collective) it returns this rank's numbers alone.  `reduce_ms_per_rank` is each rank's
+    stream time from the end of its render to the end of the collective: the xGMI reduce itself plus the wait for
+    slower ranks; `reduce_ms` is its minimum over ranks (the slowest rank waits least, so its figure is closest to the
+    transfer alone), `render_ms_max` the render of the slowest rank."""
+    import torch
+    ft = fr.frame_timings(last)
+    n = max(1, len(ft))
+    mine = [sum(f[0] for f in ft) / n, sum(f[1] for f in ft) / n]
+    if fr.collective:
+        import torch.distributed as dist
+        dev = fr.fb.device if dist.get_backend(group) == "nccl" else "cpu"
+        world = dist.get_world_size(group)
+        out = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(out, torch.tensor(mine, dtype=torch.float64, device=dev), group=group)
+        per = [[float(v) for v in t.tolist()] for t in out]
+    else:
+        per = [mine]
+    render = [p[0] for p in per]
+    reduce = [p[1] for p in per]
+    return {"frames": len(ft), "render_ms_per_rank": [round(v, 3) for v in render],
+            "reduce_ms_per_rank": [round(v, 3) for v in reduce],
+            "render_ms_max": round(max(render), 3), "reduce_ms": round(min(reduce), 3),
+            "reduce_op": fr.reduce_op if fr.collective else None}
 
 
 def reduce_framebuffers_cpu(fbs):

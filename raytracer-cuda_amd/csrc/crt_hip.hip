@@ -83,9 +83,6 @@ struct RenderParams {
     int drain_threshold;                  // variant 7: the threshold once the pixel queue is empty
     int wave_drain;                       // variants 4/8: sixty-fourths of the live lanes a draining wave passes at
     int top_levels;                       // 4-wide variants: a new ray's first node steps taken from LDS (<= CRT_TOP_LEVELS)
-    int carry_lanes, carry_max;           // variant 8 leaf-pair carry (traverse_step4c): a step's part-empty round of
-                                          // at most carry_max pairs waits for the next step when at least carry_lanes
-                                          // lanes are still traversing
 };
 
 #ifdef CRT_PROFILE_PAIRS
@@ -1065,206 +1062,6 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
     if (COUNT) cnt.cyc_round += shader_clock() - c1;
 }
 
-#ifndef CRT_LEAF_CARRY
-#define CRT_LEAF_CARRY 0
-#endif
-// Variant 8's traversal step with the leaf-pair carry (CRT_LEAF_CARRY).  traverse_step4 runs every step's pairs at
-// once, so a step with 70 pairs runs a full round and one of 6 pairs.  Here a step runs only whole rounds of 64 pairs
-// and CARRIES the part-empty remainder to the next step, whose new pairs fill it up:
-//  * `pend` = (first primitive << 8) | count of the lane's untested leaf pairs (0 = none).  A lane with a carried span
-//    takes no node step, so its `closest` stays the value the span was opened with: the same box tests, the same
-//    pairs against the same tmax, hence the same traversal as traverse_step4, bit for bit and count for count.  Only
-//    the round boundaries move, and the per-owner (t, ~rank) min (Mesh.cuh:90-103 restated, see traverse_step4) does
-//    not depend on them.
-//  * carried pairs are listed before the step's new pairs (one packed DPP scan: carried counts in the high 16 bits),
-//    so they are always in the first round: a lane waits at most one step.  A remainder is carried only when the
-//    carried pairs fit the whole rounds (so none waits twice), it holds at most carry_max pairs, and at least
-//    carry_lanes lanes are still traversing (a draining wave would not fill it); otherwise the step runs it.
-//  * a lane's LDS key stays ~0 except while its span is being tested, and is reset when its span completes, so a
-//    partly tested span keeps its running min across steps.
-template <bool COUNT>
-__device__ __forceinline__ void traverse_step4c(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
-                                                float& closest, int& hit, uint32_t& pend, TraceCounts& cnt,
-                                                WaveLdsWide& L, uint32_t* __restrict__ stk, int lane, size_t pix,
-                                                size_t n_pix) {
-    if (COUNT) cnt.step_slots++;
-    const uint64_t c0 = COUNT ? shader_clock() : 0;
-    int leaf_n, leaf_first;
-    const bool carried = pend != 0u;
-    if (carried) {
-        leaf_first = (int)(pend >> 8);
-        leaf_n = (int)(pend & 0xffu);
-    } else {
-        node_step4<COUNT>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
-    }
-    const uint64_t c1 = COUNT ? shader_clock() : 0;
-    if (COUNT) cnt.cyc_step += c1 - c0;
-    if (!wave_ballot(leaf_n > 0)) return;
-    // one scan for both lists (each sum < 64 * 256 < 2^16): carried pairs first, then the step's new pairs
-    const int incl = wave_inclusive_scan_dpp(carried ? (leaf_n << 16) : leaf_n);
-    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
-    const int total_c = (int)(tot >> 16), total = total_c + (int)(tot & 0xffffu);
-    const int pfx = carried ? (incl >> 16) - leaf_n : total_c + (incl & 0xffff) - leaf_n;
-    int limit = total & ~63;                 // whole rounds (uniform)
-    const int rem = total - limit;
-    if (rem != 0 && !(limit >= total_c && rem <= P.carry_max &&
-                      __popcll(wave_ballot(node >= 0)) >= P.carry_lanes))
-        limit = total;                       // run the remainder now
-    L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first - pfx));
-#ifdef CRT_CHECKED
-    L.prefix[lane] = pfx;
-    L.span_n[lane] = leaf_n;
-#endif
-    uint32_t carry = 0;   // owner of the last pair of the previous round (round 0 starts with a mark)
-    for (int base = 0; base < limit; base += 64) {
-        if (COUNT) cnt.round_slots++;
-        if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)(lane + 1);
-        wave_sync();
-        const uint32_t mark = L.owner_at[lane];
-        L.owner_at[lane] = 0;
-        // the span starts are not in lane order (carried spans come first), so the scan takes the LAST mark at or
-        // before this slot, not the largest owner: (slot + 1) << 6 | owner, against the previous round's last owner
-        // (slot 0, so any mark of this round beats it)
-        const uint32_t owner1 = max(wave_inclusive_max_scan_u(mark ? (((uint32_t)lane + 1u) << 6) | (mark - 1u) : 0u),
-                                    carry);
-        const int owner = (int)(owner1 & 63u);
-        const int j = base + lane;
-        if (j < limit) {
-            const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
-            const int p = __float_as_int(r1.w) + j;
-            if (COUNT) cnt.tris++;
-            int rank;
-#ifdef CRT_CHECKED
-            const bool bad = (unsigned)owner >= 64u || j < L.prefix[owner] || j >= L.prefix[owner] + L.span_n[owner] ||
-                             (unsigned)p >= (unsigned)P.n_prims;
-            if (bad) atomicOr(P.err, 4u);
-            rank = -1;
-            const float t = bad ? -1.f : prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
-                                                   P.tree_spheres != 0);
-#else
-            const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank,
-                                      P.tree_spheres != 0);
-#endif
-            const unsigned long long kp = ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank);
-            atomicMin(&L.key[owner], t >= 0.f ? kp : ~0ull);
-        }
-        carry = __builtin_amdgcn_readlane(owner1, 63) & 63u;
-        wave_sync();
-    }
-    {
-        const int done = min(max(limit - pfx, 0), leaf_n);    // this lane's pairs tested in this step's rounds
-        const bool fin = leaf_n > 0 && done == leaf_n;
-        const unsigned long long kk = L.key[lane];
-        const float t = __uint_as_float((unsigned)(kk >> 32));
-        const int rank = (int)(0xffffffffu - (unsigned)kk);
-        if (fin && kk != ~0ull && better(t, rank, closest, hit)) {
-            closest = t;
-            hit = rank;
-        }
-        L.key[lane] = fin ? ~0ull : kk;
-        pend = (leaf_n > 0 && !fin) ? (((uint32_t)(leaf_first + done) << 8) | (uint32_t)(leaf_n - done)) : 0u;
-    }
-    if (COUNT) cnt.cyc_round += shader_clock() - c1;
-}
-
-// CRT_LEAF_CARRY=2: the carry without the stall.  A lane with a carried span takes its node step too, with the
-// `closest` the span was opened with (its pairs are not folded in yet): a larger bound, so its box tests may enter
-// boxes the exact bound would cull, and their primitives are tested against that bound.  The result cannot change:
-// the hit rule is the minimum (t, ~rank) over every primitive the ray's interval reaches, a superset
-// of tested primitives holds the same minimum, and `better` merges every candidate against the current closest.  Only
-// the work counters can grow.  Two spans per lane per step: the carried one (always within round 0, whose owner
-// offsets come from the owner lane's register through ds_bpermute) and the step's new one (offsets in the LDS ray
-// record).  Each step folds its per-owner minimum into (closest, hit) and clears the key.
-// One leaf round of traverse_step4d: pairs [base, base + 64) of the step's list.  FIRST (round 0) also holds the
-// carried section [0, total_c) and takes its primitive offsets from the owners' registers; later rounds never see it,
-// so the carried span's values are dead after round 0 (peeled, so they do not stay live through the round loop).
-template <bool COUNT, bool FIRST>
-__device__ __forceinline__ void leaf_round4d(const RenderParams& P, WaveLdsWide& L, int lane, int base, int limit,
-                                             int total_c, int leaf_n, int pfx, int cn, int pfx_c, int off_c,
-                                             uint32_t& carry, TraceCounts& cnt) {
-    if (COUNT) cnt.round_slots++;
-    if (FIRST && cn > 0) L.owner_at[pfx_c] = (unsigned char)(lane + 1);
-    if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)(lane + 1);
-    wave_sync();
-    const uint32_t mark = L.owner_at[lane];
-    L.owner_at[lane] = 0;
-    // span starts are not in lane order (carried spans first): the LAST mark at or before this slot
-    const uint32_t owner1 = max(wave_inclusive_max_scan_u(mark ? (((uint32_t)lane + 1u) << 6) | (mark - 1u) : 0u), carry);
-    const int owner = (int)(owner1 & 63u);
-    const int j = base + lane;
-    int oc = 0;
-    if (FIRST && total_c > 0) oc = __builtin_amdgcn_ds_bpermute(owner << 2, off_c);   // uniform branch
-    if (j < limit) {
-        const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
-        const int p = ((FIRST && j < total_c) ? oc : __float_as_int(r1.w)) + j;
-        if (COUNT) cnt.tris++;
-        int rank;
-        const float t = prim_test(P.prims, p, v3(r0.x, r0.y, r0.z), v3(r0.w, r1.x, r1.y), r1.z, rank, P.tree_spheres != 0);
-        const unsigned long long kp = ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank);
-        atomicMin(&L.key[owner], t >= 0.f ? kp : ~0ull);
-    }
-    carry = __builtin_amdgcn_readlane(owner1, 63) & 63u;
-    wave_sync();
-}
-
-// CRT_LEAF_CARRY=2: the carry without the stall.  A lane with a carried span takes its node step too, with the
-// `closest` the span was opened with (its pairs are not folded in yet): a larger bound, so its box tests may enter
-// boxes the exact bound would cull, and their primitives are tested against that bound.  The result cannot change:
-// the hit rule is the minimum (t, ~rank) over every primitive the ray's interval reaches, a superset
-// of tested primitives holds the same minimum, and `better` merges every candidate against the current closest.  Only
-// the work counters can grow.  Two spans per lane per step: the carried one (always within round 0, whose owner
-// offsets come from the owner lane's register through ds_bpermute) and the step's new one (offsets in the LDS ray
-// record).  Each step folds its per-owner minimum into (closest, hit) and clears the key.
-template <bool COUNT>
-__device__ __forceinline__ void traverse_step4d(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
-                                                float& closest, int& hit, uint32_t& pend, TraceCounts& cnt,
-                                                WaveLdsWide& L, uint32_t* __restrict__ stk, int lane, size_t pix,
-                                                size_t n_pix) {
-    if (COUNT) cnt.step_slots++;
-    const uint64_t c0 = COUNT ? shader_clock() : 0;
-    int leaf_n, leaf_first;
-    node_step4<COUNT>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
-    const uint64_t c1 = COUNT ? shader_clock() : 0;
-    if (COUNT) cnt.cyc_step += c1 - c0;
-    const int cn = (int)(pend & 0xffu);
-    if (!wave_ballot((leaf_n | cn) > 0)) return;
-    const int incl = wave_inclusive_scan_dpp((cn << 16) | leaf_n);
-    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
-    const int total_c = (int)(tot >> 16), total = total_c + (int)(tot & 0xffffu);
-    const int pfx_c = (incl >> 16) - cn;
-    const int pfx = total_c + (incl & 0xffff) - leaf_n;
-    int limit = total & ~63;
-    const int rem = total - limit;
-    if (rem != 0 && !(limit >= total_c && rem <= P.carry_max &&
-                      __popcll(wave_ballot(node >= 0)) >= P.carry_lanes))
-        limit = total;
-    L.ray1[lane] = make_float4(d.y, d.z, closest, __int_as_float(leaf_first - pfx));
-    {
-        uint32_t ones;
-        __asm__ volatile("v_mov_b32 %0, -1" : "=v"(ones));
-        L.key[lane] = ((unsigned long long)ones << 32) | ones;
-    }
-    if (limit > 0) {
-        uint32_t carry = 0;
-        leaf_round4d<COUNT, true>(P, L, lane, 0, limit, total_c, leaf_n, pfx, cn, pfx_c, (int)(pend >> 8) - pfx_c, carry,
-                                  cnt);
-        for (int base = 64; base < limit; base += 64)
-            leaf_round4d<COUNT, false>(P, L, lane, base, limit, total_c, leaf_n, pfx, 0, 0, 0, carry, cnt);
-    }
-    {
-        const int done = min(max(limit - pfx, 0), leaf_n);
-        const unsigned long long kk = L.key[lane];
-        const float t = __uint_as_float((unsigned)(kk >> 32));
-        const int rank = (int)(0xffffffffu - (unsigned)kk);
-        if (kk != ~0ull && better(t, rank, closest, hit)) {
-            closest = t;
-            hit = rank;
-        }
-        pend = (leaf_n > done) ? (((uint32_t)(leaf_first + done) << 8) | (uint32_t)(leaf_n - done)) : 0u;
-    }
-    if (COUNT) cnt.cyc_round += shader_clock() - c1;
-}
-
 // The tree's top nodes held in LDS (CRT_TOP_LEVELS): the root and, at level 2, its internal children, copied once
 // per workgroup with their rows unswizzled (row k at 16-B slot k).  Every ray starts at the root, and its first node
 // steps are the same for every ray up to the direction signs, so a new ray takes them in the regeneration pass from
@@ -1783,16 +1580,12 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         uint32_t rows = 0;         // ray_rows(inv)
         L.owner_at[lane] = 0;      // traverse_step4: owner + 1, 0 = none
         if (TILED && lane == 0) L.rays = 0;
-        constexpr bool CARRY = TILED && CRT_LEAF_CARRY != 0;
-        uint32_t pend = 0;         // traverse_step4c: the lane's carried leaf span, 0 = none
-        if (CARRY) L.key[lane] = ~0ull;
         // variant 8: the most expensive tiles of the cost order bound the frame when it has few tiles per wave slot
         // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
         const int regen_t = (TILED && (int)blockIdx.x < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
         bool first_pass = true;    // uniform
         for (;;) {
-            // a lane whose trace ended but whose carried leaf pairs are untested is not parked yet
-            const uint64_t parked_mask = live_mask & wave_ballot(CARRY ? (node < 0 && pend == 0u) : node < 0);
+            const uint64_t parked_mask = live_mask & wave_ballot(node < 0);
             const int n_parked = __popcll(parked_mask);
             const int n_live = __popcll(live_mask);
             if (n_live == 0) break;
@@ -1845,15 +1638,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
-            if constexpr (CARRY && CRT_LEAF_CARRY == 2)
-                traverse_step4d<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, pend, cnt, L, stk, lane,
-                                       (size_t)pix, n_pix);
-            else if constexpr (CARRY)
-                traverse_step4c<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, pend, cnt, L, stk, lane,
-                                       (size_t)pix, n_pix);
-            else
-                traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix,
-                                      n_pix);
+            traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
         }
     } else if constexpr (VARIANT == 2 || VARIANT == 3 || VARIANT == 10) {
         constexpr bool PF = VARIANT == 3 || VARIANT == 10;
@@ -2917,10 +2702,12 @@ struct crt_renderer {
     // HIP events of the current render: ev0 before the cost probe, ev_main just before the main render kernel (after
     // the probe and the tile sort), ev1 after it.  They point into a ring of CRT_TIMING_RING frames, so a caller that
     // renders K frames back to back without synchronising can read every frame's phases afterwards
-    // (crt_renderer_timing_history).
+    // (crt_renderer_timing_history).  The ring has one slot more than the history reaches: a render records into slot
+    // n_timed % (CRT_TIMING_RING + 1), which none of the last CRT_TIMING_RING complete frames occupies, so a render that
+    // fails after its first event (an allocation, the overflow-region check) leaves every readable slot intact.
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_main = nullptr;
-    hipEvent_t ring[CRT_TIMING_RING][3] = {};
+    hipEvent_t ring[CRT_TIMING_RING + 1][3] = {};
     unsigned long long n_timed = 0;   // renders whose three events were all recorded
     char kernel_name[64] = "";     // instantiation of the last render launch, rocprof's spelling
     // variant 7: pixel order, slot queue, probe costs, sort scratch (allocated on first use)
@@ -2946,7 +2733,6 @@ struct crt_renderer {
     int tile_shard = 0, tile_shards = 1;   // pixel sharding (crt_renderer_set_pixel_shard)
     int crit_threshold = 16;       // (measured: profiles/r02h, r02i)
     int top_levels = -1;           // 4-wide variants: new rays' first node steps from LDS; -1 = CRT_TOP_LEVELS
-    int carry_lanes = 16, carry_max = 63;   // variant 8 leaf-pair carry (builds with CRT_LEAF_CARRY)
     int xcd_regions = 0;           // variant 8: XCD groups render screen strips (crt_xcd_order_kernel)
     int probe_stride = 0;          // variant 8's cost probe: every probe_stride-th pixel in x and y (0 = automatic)
     int temporal = 0;              // variant 7: tiles ordered by the previous variant-7 frame's rays per pixel
@@ -3376,12 +3162,12 @@ int crt_renderer_set_kernel_variant(crt_renderer* R, int variant) {
 
 int crt_renderer_set_schedule(crt_renderer* R, int probe_spp, int min_spp, int flags) {
     if (!R || probe_spp < -1 || probe_spp > 64 || min_spp < 0) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad schedule");
+    const int stride = (flags >> 20) & 0xf;   // variant 8's probe subsampling: 0 = automatic, 1 (every pixel), 2, 4
+    if (stride != 0 && stride != 1 && stride != 2 && stride != 4)   // checked before any field changes
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "probe stride (flags >> 20): 0, 1, 2 or 4");
     R->probe_spp = probe_spp < 0 ? -1 : probe_spp;
     R->probe_min_spp = min_spp;
     R->tile_key_mode = (flags >> 16) & 0xf;   // 0 = slowest pixel (callers that pass 0 get the plain key)
-    const int stride = (flags >> 20) & 0xf;   // variant 8's probe subsampling: 0 = automatic, 1 (every pixel), 2, 4
-    if (stride != 0 && stride != 1 && stride != 2 && stride != 4)
-        return set_error(CRT_ERR_INVALID_ARGUMENT, "probe stride (flags >> 20): 0, 1, 2 or 4");
     R->probe_stride = stride;
     return CRT_OK;
 }
@@ -3467,8 +3253,6 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.ovf = nullptr;
     P.order = nullptr; P.queue = nullptr; P.n_slots = 0; P.probe_cost = nullptr; P.tiles_x = 0; P.crit_tiles = 0; P.crit_threshold = 64;
     P.top_levels = R->top_levels < 0 ? CRT_TOP_LEVELS : R->top_levels;
-    P.carry_lanes = R->carry_lanes;
-    P.carry_max = R->carry_max;
     P.stack_cap = S->stack_cap;
     P.sphere_first = S->sphere_first;
     P.n_ray_spheres = S->n_ray_spheres;
@@ -3490,9 +3274,8 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         if (P.accumulate) return set_error(CRT_ERR_INVALID_ARGUMENT, "pixel sharding does not accumulate");
         HIP_TRY(hipMemsetAsync(R->d_sum, 0, (size_t)R->width * R->height * 3 * sizeof(float), st));
     }
-    {   // this render's slot of the timing ring: the oldest frame's, so a render that fails half-way never touches
-        // the slot of the last complete frame
-        hipEvent_t* slot = R->ring[R->n_timed % CRT_TIMING_RING];
+    {   // this render's slot of the timing ring: the spare slot, which no readable frame occupies (crt_renderer)
+        hipEvent_t* slot = R->ring[R->n_timed % (CRT_TIMING_RING + 1)];
         R->ev0 = slot[0]; R->ev_main = slot[1]; R->ev1 = slot[2];
     }
     HIP_TRY(hipEventRecord(R->ev0, st));
@@ -3968,7 +3751,7 @@ int crt_renderer_timing_history(crt_renderer* R, int back, float out[3]) {
     if (!R || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
     if (back < 0 || back >= CRT_TIMING_RING) return set_error(CRT_ERR_INVALID_ARGUMENT, "back outside [0, CRT_TIMING_RING)");
     if ((unsigned long long)back >= R->n_timed) return set_error(CRT_ERR_INVALID_ARGUMENT, "fewer renders than back + 1");
-    hipEvent_t* slot = R->ring[(R->n_timed - 1 - (unsigned long long)back) % CRT_TIMING_RING];
+    hipEvent_t* slot = R->ring[(R->n_timed - 1 - (unsigned long long)back) % (CRT_TIMING_RING + 1)];
     HIP_TRY(hipSetDevice(R->device));
     HIP_TRY(hipEventSynchronize(slot[2]));
     HIP_TRY(hipEventElapsedTime(&out[0], slot[0], slot[2]));
@@ -4002,13 +3785,14 @@ int crt_renderer_set_xcd_regions(crt_renderer* R, int on) {
     return CRT_OK;
 }
 
+// The round-4 leaf-pair carry was measured and not kept (+1.8 % / +15 %); its kernels live on as
+// profiles/r04c/leaf_carry.patch.  The entry point stays in the ABI and reports that this build has no carry.
 int crt_renderer_set_leaf_carry(crt_renderer* R, int lanes, int max_pairs) {
     if (!R) return set_error(CRT_ERR_INVALID_ARGUMENT, "null renderer");
-    if (lanes < 0 || lanes > 65 || max_pairs < 0 || max_pairs > 63)
-        return set_error(CRT_ERR_INVALID_ARGUMENT, "leaf carry: lanes in [0, 65], max_pairs in [0, 63]");
-    R->carry_lanes = lanes;
-    R->carry_max = max_pairs;
-    return CRT_OK;
+    (void)lanes;
+    (void)max_pairs;
+    return set_error(CRT_ERR_UNSUPPORTED, "leaf-pair carry: not in this build (measured and removed, DESIGN.md §8; "
+                                          "profiles/r04c/leaf_carry.patch)");
 }
 
 int crt_renderer_last_timings(crt_renderer* R, float out[3]) {

@@ -162,6 +162,60 @@ def test_gloo_pixel_shards_equal_the_unsharded_frame(scenes, world):
     assert res[0][4] == np.float32(1) / np.float32(SPP)
 
 
+def _timing_worker(rank, world, port, files, q):
+    """Two frames of the sharded path, then the per-rank timings bench.py puts in its N > 1 line; then an unsharded
+    (world 1) frame inside the same 2-rank job, which must stay local (no collective over the default group)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import objload
+    import pyoracle
+    from crt_amd.dist import gather_frame_timings
+    o = pyoracle.OracleScene(objload.load_scene(files))
+    r = OracleShardRenderer(o, pyoracle.camera(), W, H)
+    fr = ShardedFrameRenderer(r, None, SPP, 20, 41, rank, world, reduce_op="reduce", fb_device="cpu")
+    fr.render()
+    fr.render()
+    t = gather_frame_timings(fr, last=2)
+    r1 = OracleShardRenderer(o, pyoracle.camera(), W, H)
+    solo = ShardedFrameRenderer(r1, None, SPP, 20, 41, rank, 1, fb_device="cpu")
+    solo_collective = solo.collective
+    if rank == 0:   # only rank 0 renders it: a collective here would hang the job
+        solo.render()
+    mismatch = None
+    try:
+        ShardedFrameRenderer(r1, None, SPP, 20, 41, rank, 1, fb_device="cpu", collective=True)
+    except ValueError as e:
+        mismatch = str(e)
+    q.put((rank, t, solo_collective, mismatch))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_n2_line_carries_per_rank_timings(scenes):
+    """bench.py's N > 1 keys (render_ms_per_rank, reduce_ms, ...) come from gather_frame_timings: every rank gets all
+    ranks' averages; a world-1 frame inside a larger job stays local (dist.py collective auto-enable)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_timing_worker, args=(r, 2, port, scenes["cornell"], q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in ps], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, t, solo_collective, mismatch in res:
+        for k in ("render_ms_per_rank", "reduce_ms_per_rank", "render_ms_max", "reduce_ms", "frames", "reduce_op"):
+            assert k in t
+        assert t["frames"] == 2 and t["reduce_op"] == "reduce"
+        assert len(t["render_ms_per_rank"]) == 2 and len(t["reduce_ms_per_rank"]) == 2
+        assert all(v > 0 for v in t["render_ms_per_rank"]) and all(v >= 0 for v in t["reduce_ms_per_rank"])
+        assert t["render_ms_max"] == max(t["render_ms_per_rank"])
+        assert solo_collective is False
+        assert mismatch is not None and "2 ranks" in mismatch
+    assert res[0][1] == res[1][1]   # all_gather: both ranks hold the same table
+
+
 def test_pixel_mode_argument_checks():
     with pytest.raises(ValueError):
         ShardedFrameRenderer(None, None, 8, mode="rows")

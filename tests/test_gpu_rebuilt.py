@@ -331,6 +331,80 @@ def test_shipped_instantiation_against_the_oracle(rebuilt, oracle_scenes):
     assert c["rays"] / (240 * 4 * spp) > 1.15 * per_sample[950], (c["rays"], per_sample)
 
 
+def _shipped_frame(dev, w, h, spp, kernel):
+    """A frame through the automatic choice (probe, tile sort, critical tiles), asserting the instantiation it ran."""
+    cam = crt_amd.camera(spp)
+    r = crt_amd.Renderer(w, h)
+    r.set_camera(cam)
+    r.init_rand(41)
+    r.render(dev, spp, 20)
+    r.resolve(crt_amd.pixel_sample_scale(spp))
+    r.synchronize()
+    assert r.last_kernel_name() == kernel
+    ph = r.last_timings()
+    assert ph["probe_sort_ms"] > 0 and ph["main_kernel_ms"] > 0          # the probe and the sort ran before the kernel
+    return r, crt_amd.camera_floats(cam)
+
+
+@pytest.fixture(scope="module")
+def config_e():
+    """Config E (BASELINE.json configs[4]): Cornell + one OBJ of ten translated ~100k-triangle glass bunny proxies;
+    the device scene as bench.py builds it (GPU mesh BVH, GPU binned-SAH 4-wide tree) and the oracle's own load."""
+    import objload
+    import pyoracle
+    from crt_amd import assets
+    files = assets.scene_files("cornell_1m")
+    hs = crt_amd.HostScene(files, build_device=0)
+    dev = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
+    return dev, pyoracle.OracleScene(objload.load_scene(files))
+
+
+# Config E's ten bunnies project onto rows ~80-320 (row 0 = bottom) and columns ~800-1760 of the 2560x1440 frame (their
+# vertices through the bench camera); the y0 = 200 band crosses all of them.
+BANDS_E = (200, 264, 700, 1300)
+
+
+def test_config_e_shipped_instantiation_against_the_oracle(config_e):
+    """Config E's benchmarked kernel against the oracle directly (the deep-BVH config, Mesh.cuh:55-110): the 1M-triangle
+    scene at 2560x1440 and 64 spp through the automatic choice, which runs the cost probe and the tile sort and launches
+    crt_render_kernel<false, 8, 7>.  Four full-width 4-row bands, two through the instanced glass bunnies, rendered by
+    the oracle (CUDAKernels.h:147-166 restated, the reference's own median-split BVH) from the same RNG streams; each
+    band holds the north-star bar (per-channel RMS <= 1e-4) with >= 99.9 % of its pixels bit-identical."""
+    dev, osc = config_e
+    w, h, spp = 2560, 1440, 64
+    r, cf = _shipped_frame(dev, w, h, spp, "crt_render_kernel<false, 8, 7>")
+    lin, rgba = r.linear(), r.rgba8()
+    nt = _usable_cores()
+    for y0 in BANDS_E:
+        o_sum, o_rgba, o_cnt = osc.render(cf, w, h, spp, 20, rect=(0, y0, w, y0 + 4), nthreads=nt)
+        _compare(lin[y0:y0 + 4], o_sum, spp, 0.999)
+        assert np.mean(np.all(rgba[y0:y0 + 4] == o_rgba, axis=-1)) >= 0.999
+    # the bunny band really crosses the mesh: its rays descend the reference's mesh BVH much deeper than a wall band's
+    # (oracle counters here: 23.7 against 17.3 box tests per ray at 4 spp)
+    _, _, c_b = osc.render(cf, w, h, 4, 20, rect=(800, 200, 1760, 204), nthreads=nt)
+    _, _, c_w = osc.render(cf, w, h, 4, 20, rect=(0, 1300, 400, 1304), nthreads=nt)
+    assert c_b["box_tests"] / c_b["rays"] > 1.2 * c_w["box_tests"] / c_w["rays"], (c_b, c_w)
+
+
+BANDS_B_FULL = (4, 352, 488, 716)      # full-width 4-row bands of config B; y0 = 488 crosses the glass bunny
+
+
+def test_config_b_shipped_instantiation_against_the_oracle(rebuilt, oracle_scenes):
+    """Config B's benchmarked kernel (1280x720, 256 spp: 2 tiles per wave slot, so crt_render_kernel<false, 8, 6>) against
+    the oracle directly, not against the reference-BVH GPU frame: four full-width bands at the full 256 spp, one through
+    the glass bunny, each within the north-star bar with >= 99.9 % of its pixels bit-identical."""
+    dev = rebuilt["cornell_bunny", "w4"]
+    w, h, spp = 1280, 720, 256
+    r, cf = _shipped_frame(dev, w, h, spp, "crt_render_kernel<false, 8, 6>")
+    lin, rgba = r.linear(), r.rgba8()
+    nt = _usable_cores()
+    osc = oracle_scenes["cornell_bunny"]
+    for y0 in BANDS_B_FULL:
+        o_sum, o_rgba, _ = osc.render(cf, w, h, spp, 20, rect=(0, y0, w, y0 + 4), nthreads=nt)
+        _compare(lin[y0:y0 + 4], o_sum, spp, 0.999)
+        assert np.mean(np.all(rgba[y0:y0 + 4] == o_rgba, axis=-1)) >= 0.999
+
+
 @pytest.mark.parametrize("w,h,spp", [(640, 360, 64), (100, 37, 70), (2560, 1440, 64)])
 def test_xcd_regions_are_bit_identical(rebuilt, w, h, spp):
     """Variant 8 with the XCD-region tile order (crt_renderer_set_xcd_regions: blocks b and b + 8 render one screen

@@ -39,7 +39,7 @@ ab)
   LIBB=$1; N=${2:-2}; shift 2
   for i in $(seq 1 $N); do
     timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-count --no-parity "$@" > $R/$OUT/bench_A$i.log 2>&1
-    CRT_HIP_LIB=$R/$LIBB timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-count --no-parity "$@" \
+    CRT_SKIP_ABI_CHECK=1 CRT_HIP_LIB=$R/$LIBB timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-count --no-parity "$@" \
         > $R/$OUT/bench_B$i.log 2>&1
   done
   ;;
@@ -60,7 +60,7 @@ libs)
     echo "A round $i: $(grep -o '"render_kernel_ms_avg": [0-9.]*' $R/$OUT/A_$i.log)"
     for lib in "$@"; do
       label=$(basename $(dirname $lib))
-      CRT_HIP_LIB=$R/$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-count --no-parity > $R/$OUT/${label}_$i.log 2>&1
+      CRT_SKIP_ABI_CHECK=1 CRT_HIP_LIB=$R/$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-count --no-parity > $R/$OUT/${label}_$i.log 2>&1
       echo "$label round $i: $(grep -o '"render_kernel_ms_avg": [0-9.]*' $R/$OUT/${label}_$i.log)"
     done
   done
