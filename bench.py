@@ -119,9 +119,6 @@ def parse():
                     help="variants 4/8: a draining wave passes at this many 64ths of its live lanes (64 = all)")
     ap.add_argument("--drain-threshold", type=int, default=None,
                     help="variant 7: regeneration threshold once the pixel queue is empty (0 = unchanged)")
-    ap.add_argument("--tail-lanes", type=int, default=None,
-                    help="variant 8: a wave whose live lanes drop to this many finishes them in the per-lane tail loop "
-                         "(crt_renderer_set_tail_mode; 0 = off; default: the library's)")
     ap.add_argument("--xcd-regions", type=int, default=None, choices=[0, 1],
                     help="variant 8: XCD groups render equal-cost screen strips (crt_renderer_set_xcd_regions)")
     ap.add_argument("--bvh", default="rebuilt", choices=["rebuilt", "reference"])
@@ -399,8 +396,6 @@ def main():
             rr.set_drain_threshold(args.drain_threshold)
         if args.wave_drain is not None:
             rr.set_wave_drain(args.wave_drain)
-        if args.tail_lanes is not None:
-            rr.set_tail_mode(args.tail_lanes)
         rr.set_camera(cam)
         return rr
 

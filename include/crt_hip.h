@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CRT_ABI_VERSION 4
+#define CRT_ABI_VERSION 3
 
 enum crt_status {
     CRT_OK = 0,
@@ -285,11 +285,6 @@ int  crt_renderer_set_drain_threshold(crt_renderer* r, int lanes);
  * runs when `sixty_fourths`/64 of those live lanes are parked (1..64; 64 = only when all of them are; default 48), so
  * the wave's last pixels wait less for each other's paths.  Results never depend on it. */
 int  crt_renderer_set_wave_drain(crt_renderer* r, int sixty_fourths);
-/* Variant 8 tail mode: once at most `lanes` (0..64; 0 = off) of a wave's lanes still have samples, each finishes its
- * pixel on its own -- node steps, its own leaf span tested in the lane, its end of trace shaded as soon as it parks --
- * instead of the cooperative leaf rounds and the regeneration threshold.  Same traversal, tests and hit rule, so
- * results (frames, RNG state, ray and work counts) never depend on it. */
-int  crt_renderer_set_tail_mode(crt_renderer* r, int lanes);
 /* Variant 8 with the cost probe: 1 = the blocks that share an XCD (block index mod 8, MI355X's round-robin dispatch)
  * render one screen strip of equal probe cost, most expensive tile first, so each XCD's L2 holds its strip's geometry;
  * 0 = one global cost order (default).  Ignored with pixel sharding.  Results never depend on it. */

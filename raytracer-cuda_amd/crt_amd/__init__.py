@@ -318,11 +318,6 @@ class Renderer:
         """Variant 7: regeneration threshold once the pixel queue is empty, 0 = unchanged (crt_renderer_set_drain_threshold)."""
         check(_lib.hip().crt_renderer_set_drain_threshold(self.h, int(lanes)), "set_drain_threshold")
 
-    def set_tail_mode(self, lanes: int):
-        """Variant 8: a wave with at most `lanes` live lanes finishes them one lane at a time (crt_renderer_set_tail_mode;
-        0 = off).  Results never depend on it."""
-        check(_lib.hip().crt_renderer_set_tail_mode(self.h, int(lanes)), "set_tail_mode")
-
     def set_wave_drain(self, sixty_fourths: int):
         """Variants 4/8: a draining wave passes at sixty_fourths/64 of its live lanes (crt_renderer_set_wave_drain)."""
         check(_lib.hip().crt_renderer_set_wave_drain(self.h, int(sixty_fourths)), "set_wave_drain")

@@ -82,8 +82,6 @@ struct RenderParams {
                                           // crit_threshold parked lanes instead of regen_threshold
     int drain_threshold;                  // variant 7: the threshold once the pixel queue is empty
     int wave_drain;                       // variants 4/8: sixty-fourths of the live lanes a draining wave passes at
-    int tail_lanes;                       // variant 8: a wave with at most this many live lanes finishes them in the
-                                          // per-lane tail loop (0 = never; crt_renderer_set_tail_mode)
     int top_levels;                       // 4-wide variants: a new ray's first node steps taken from LDS (<= CRT_TOP_LEVELS)
 };
 
@@ -1005,9 +1003,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         // the loop and spills it (a scratch reload and a vmcnt(0) wait on every leaf step)
         uint32_t ones;
         __asm__ volatile("v_mov_b32 %0, -1" : "=v"(ones));
-        // the key's address from the lane id at the point of use (lane_fresh): with the tail step in the loop the
-        // allocator otherwise keeps &L.key[lane] in a scratch slot and reloads it on every leaf step
-        L.key[lane_fresh()] = ((unsigned long long)ones << 32) | ones;
+        L.key[lane] = ((unsigned long long)ones << 32) | ones;
     }
     uint32_t carry = 0;   // owner + 1 of the last pair of the previous round
     for (int base = 0; base < total; base += 64) {
@@ -1055,7 +1051,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         wave_sync();
     }
     {
-        const unsigned long long kk = L.key[lane_fresh()];
+        const unsigned long long kk = L.key[lane];
         const float t = __uint_as_float((unsigned)(kk >> 32));
         const int rank = (int)(0xffffffffu - (unsigned)kk);
         if (leaf_n > 0 && kk != ~0ull && better(t, rank, closest, hit)) {
@@ -1064,30 +1060,6 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         }
     }
     if (COUNT) cnt.cyc_round += shader_clock() - c1;
-}
-
-// Variant 8's tail mode (crt_renderer_set_tail_mode): one step of a lane that runs alone.  The node step is
-// node_step4's; the hit leaf children's primitives are tested in the lane, in order, against the closest hit at the
-// step's start -- the tmax the leaf rounds use -- and folded in with better(), which keeps the minimum (t, ~rank) in any
-// order.  No pair scan, owner marks, LDS ray record or round syncs, so a wave of a few lanes steps faster; the box
-// tests, the primitive tests and the hit are those of traverse_step4, bit for bit and count for count.
-template <bool COUNT>
-__device__ __forceinline__ void tail_step4(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
-                                           float& closest, int& hit, TraceCounts& cnt, uint32_t* __restrict__ stk,
-                                           int lane, size_t pix, size_t n_pix) {
-    if (COUNT) cnt.step_slots++;
-    int leaf_n, leaf_first;
-    node_step4<COUNT>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
-    const float tmax = closest;
-    for (int j = 0; j < leaf_n; ++j) {
-        if (COUNT) cnt.tris++;
-        int rank;
-        const float t = prim_test(P.prims, leaf_first + j, o, d, tmax, rank, P.tree_spheres != 0);
-        if (t >= 0.f && better(t, rank, closest, hit)) {
-            closest = t;
-            hit = rank;
-        }
-    }
 }
 
 // The tree's top nodes held in LDS (CRT_TOP_LEVELS): the root and, at level 2, its internal children, copied once
@@ -1612,21 +1584,17 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
         const int regen_t = (TILED && (int)blockIdx.x < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
         bool first_pass = true;    // uniform
-        bool tail = false;         // uniform: tail mode reached (variant 8)
         for (;;) {
             const uint64_t parked_mask = live_mask & wave_ballot(node < 0);
             const int n_parked = __popcll(parked_mask);
             const int n_live = __popcll(live_mask);
             if (n_live == 0) break;
-            // tail mode (crt_renderer_set_tail_mode): the wave's last few lanes each run alone (tail_step4), and a lane
-            // is shaded as soon as it parks
-            if (TILED && n_live <= P.tail_lanes) tail = true;
             const uint64_t c0 = COUNT ? shader_clock() : 0;
             // once fewer than regen_t lanes still have samples, waiting for every live lane to park before a pass makes
             // each of them wait for the slowest path of the others at every bounce; a pass at wave_drain/64 of them
             // (crt_renderer_set_wave_drain; 64 = all) shortens the wave's own drain (profiles/r04n)
             const bool drain_pass = n_live < regen_t && n_parked * 64 >= n_live * P.wave_drain;
-            if (n_parked >= regen_t || n_parked == n_live || drain_pass || (TILED && tail && n_parked > 0)) {
+            if (n_parked >= regen_t || n_parked == n_live || drain_pass) {
                 if (COUNT) cnt.passes++;
                 if (__builtin_amdgcn_inverse_ballot_w64(parked_mask)) {
                     const uint64_t s0 = COUNT ? shader_clock() : 0;
@@ -1670,11 +1638,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
-            if (TILED && tail)
-                tail_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, stk, lane, (size_t)pix, n_pix);
-            else
-                traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix,
-                                      n_pix);
+            traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
         }
     } else if constexpr (VARIANT == 2 || VARIANT == 3 || VARIANT == 10) {
         constexpr bool PF = VARIANT == 3 || VARIANT == 10;
@@ -2774,7 +2738,6 @@ struct crt_renderer {
     int temporal = 0;              // variant 7: tiles ordered by the previous variant-7 frame's rays per pixel
     int drain_threshold = 0;       // variant 7: regeneration threshold once the pixel queue is empty (0 = unchanged)
     int wave_drain = 48;           // variants 4/8: draining waves pass at 48/64 of their live lanes (profiles/r04n)
-    int tail_lanes = 0;            // variant 8: per-lane tail loop at <= tail_lanes live lanes (0 = off)
     uint32_t* d_pix_rays = nullptr;   // variant 7 with the temporal order: rays per pixel of the last frame
     uint32_t* d_tile_order = nullptr; // its tiles, most expensive first
     bool pix_rays_valid = false;
@@ -3302,7 +3265,6 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.regen_threshold = S->width == 4 ? R->regen_threshold_wide : R->regen_threshold;
     P.drain_threshold = R->drain_threshold > 0 ? R->drain_threshold : P.regen_threshold;
     P.wave_drain = R->wave_drain;
-    P.tail_lanes = R->tail_lanes;
     if (R->tile_shards > 1) {
         // pixel sharding: variant 8 renders this shard's tiles; every other pixel of the framebuffer is 0, so the sum
         // of the shards' framebuffers (one collective) is the unsharded frame exactly (x + 0 = x).  Checked and
@@ -3814,12 +3776,6 @@ int crt_renderer_set_drain_threshold(crt_renderer* R, int lanes) {
 int crt_renderer_set_wave_drain(crt_renderer* R, int sixty_fourths) {
     if (!R || sixty_fourths < 1 || sixty_fourths > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "wave drain 1..64");
     R->wave_drain = sixty_fourths;
-    return CRT_OK;
-}
-
-int crt_renderer_set_tail_mode(crt_renderer* R, int lanes) {
-    if (!R || lanes < 0 || lanes > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "tail lanes 0..64");
-    R->tail_lanes = lanes;
     return CRT_OK;
 }
 

@@ -442,37 +442,6 @@ def test_probe_stride_is_bit_identical(rebuilt, stride):
         assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1]) and out[0][2] == out[1][2]
 
 
-@pytest.mark.parametrize("config", ["w4", "w4sbvh"])
-def test_tail_mode_is_bit_identical(rebuilt, config):
-    """Variant 8's tail mode (crt_renderer_set_tail_mode): the last few lanes of a wave run alone (their own leaf spans,
-    shaded as soon as they park).  The traversal and the tests are the cooperative loop's, so frames, RNG state, the ray
-    count and the counting kernel's box / triangle / sphere tests equal tail mode off -- at 64 lanes the whole wave runs in
-    the tail loop from its first pass; ragged sizes and occupancy 6 and 7 (the 640x360 frame is under 4 tiles per slot)
-    included; the SBVH tree has duplicated triangle references."""
-    dev = rebuilt["cornell_bunny", config]
-    for w, h, spp in ((640, 360, 64), (100, 37, 70), (2560, 1440, 8)):
-        out = []
-        for tl in (0, 4, 16, 64):
-            r = crt_amd.Renderer(w, h)
-            r.set_kernel_variant(8)
-            r.set_tail_mode(tl)
-            r.set_camera(crt_amd.camera(spp))
-            r.init_rand(41)
-            r.render(dev, spp, 20)
-            r.synchronize()
-            assert r.last_kernel_name().startswith("crt_render_kernel<false, 8,")
-            got = (r.linear().view(np.uint32), r.rng_state(), r.counters()["rays"])
-            r.init_rand(41)
-            r.render(dev, spp, 20, count_work=True)
-            r.synchronize()
-            c = r.counters()
-            out.append(got + ((c["rays"], c["box_tests"], c["tri_tests"], c["sphere_tests"], c["paths"]),))
-        for o in out[1:]:
-            assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1]) and out[0][2] == o[2]
-            assert out[0][3] == o[3], (out[0][3], o[3])
-        assert out[0][3][0] == out[0][2]
-
-
 def test_wave_drain_is_bit_identical(rebuilt):
     """Variants 8 and 4 with draining waves passing at 16/64 and 48/64 (the default) of their live lanes instead of all
     of them (crt_renderer_set_wave_drain): only when lanes run their shading passes changes, so frames, RNG state and ray

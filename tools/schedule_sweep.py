@@ -5,7 +5,7 @@ that share `reps` times, the settings interleaved round by round, and prints per
 time (best and median), the render with the probe and tile sort, and the rays.  Settings are
 `name:key=value,key=value` with keys crit (critical tiles, -1 = auto), lanes (their threshold), T (regeneration
 threshold), occ (waves per SIMD, 0 = auto), stride (probe stride, 0 = auto), probe (probe spp, -1 = auto), wd (the wave
-drain in 64ths, crt_renderer_set_wave_drain), tail (variant 8's tail-mode lanes, crt_renderer_set_tail_mode).  Results
+drain in 64ths, crt_renderer_set_wave_drain).  Results
 never depend on them; the ray count is printed so that a setting that changed the work would show.
 
     python tools/schedule_sweep.py --world 8 --set base: crit0:crit=0 crit2k:crit=2048 T40:T=40 occ6:occ=6
@@ -34,7 +34,7 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--set", nargs="+", default=["base:"])
 a = ap.parse_args()
 
-DEFAULT = {"crit": -1, "lanes": 16, "T": 44, "occ": 0, "stride": 0, "probe": -1, "wd": 48, "tail": 0}
+DEFAULT = {"crit": -1, "lanes": 16, "T": 44, "occ": 0, "stride": 0, "probe": -1, "wd": 48}
 settings = []
 for s in a.set:
     name, _, kv = s.partition(":")
@@ -61,7 +61,6 @@ def run(d: dict) -> dict:
     r.set_regen_threshold(d["T"])
     r.set_occupancy_target(d["occ"])
     r.set_wave_drain(d["wd"])
-    r.set_tail_mode(d["tail"])
     r.init_rand(41, base)
     r.render(sc, spp, a.bounces)
     r.synchronize()
