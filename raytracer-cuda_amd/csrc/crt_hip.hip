@@ -774,9 +774,12 @@ __device__ __forceinline__ void ray_spheres2(const float* sa, const float* sb, V
     }
     if (!(reach[0] || reach[1])) return;
     const float qa = dot(d, d);
-    float t[2];
+    float t[2] = {-1.f, -1.f};
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
+        // a sphere no lane of the wave reaches skips its quadratic (a wave-uniform branch): the small metal sphere of the
+        // benchmark scenes is outside most waves' rays, while the ground sphere's box holds every downward ray
+        if (__builtin_amdgcn_ballot_w64(reach[s]) == 0) continue;
         const float4 c = *reinterpret_cast<const float4*>(sp[s]);
         const float ocx = o.x - c.x, ocy = o.y - c.y, ocz = o.z - c.z;
         const float hb = (ocx * d.x + ocy * d.y) + ocz * d.z;
@@ -924,12 +927,15 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
             const int hi = (int)((ends >> (8u * last)) & 0xffu);
             leaf_n = hi - lo;
             leaf_first = __float_as_int(mf.z) + lo;
-            // the span must lie inside the primitive array: checked here once per lane and step instead of per pair
-            // in the leaf rounds (-0.7 %, profiles/r02v); a corrupt node reports through P.err and tests nothing
+#ifdef CRT_CHECKED
+            // the span must lie inside the primitive array.  emit4 guarantees it for every node it writes (checked there
+            // on the host, once per node), so the fast build trusts the tree; the checked build re-checks it here once per
+            // lane and step (before round 5 the fast build did too: one kernel-argument reload and wait per leaf step)
             if ((unsigned)leaf_first > (unsigned)P.n_prims || (unsigned)leaf_n > (unsigned)(P.n_prims - leaf_first)) {
                 atomicOr(P.err, 1u);
                 leaf_n = 0;
             }
+#endif
         }
         uint32_t k[4];
 #pragma unroll
@@ -1635,7 +1641,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 live_mask = wave_ballot(has_result);
                 first_pass = false;
                 // variant 8 counts the wave's rays in LDS (one VGPR less in the hot loop)
-                if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);
+                // (an LDS add without return: a read-modify-write made the wave wait for the read at every pass)
+                if (TILED && lane == 0) atomicAdd(&L.rays, (uint32_t)__popcll(parked_mask & live_mask));
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
             traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
@@ -2609,6 +2616,9 @@ private:
             if (prims.size() / 3 >= ((size_t)1 << 24)) { err = "the 4-wide tree holds at most 2^24 - 1 primitives"; return false; }
             // node_step4 takes the leaf span from counts * 0x01010101 (byte-wise running sums)
             if (total_leaf > 255) { err = "leaf children of one node hold more than 255 primitives"; return false; }
+            // every span node_step4 can form lies inside the primitive array: the fast kernel relies on it (the checked
+            // build re-checks it on the device)
+            if ((size_t)leaf_first + (size_t)total_leaf > prims.size() / 3) { err = "leaf span outside the primitives"; return false; }
             float row[6][4];
             for (int s = 0; s < 4; ++s) {
                 for (int a = 0; a < 3; ++a) {

@@ -1,19 +1,25 @@
 #!/bin/bash
 # The current one-off GPU job (overwritten per job; the copy that ran is kept as profiles/<id>/job.sh).
-# r05c: variant 8's tail mode (crt_renderer_set_tail_mode): bit-identity tests, then tail lanes 0/2/4/8/16 interleaved
-# on config B (1280x720, 256 spp), config C (2000 spp) and the N = 8 rank share (250 spp).
+# r05d: pass / step micro-changes (a wave-uniform skip of a per-ray sphere no lane reaches, the wave's ray count by an
+# LDS add without return, the leaf-span bounds check moved from every leaf step to the host's emission) against the
+# previous commit (lib_exp/base): bit identity (tools/frame_hash.py), then interleaved main-kernel times on C, B and E.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=r05c; OUT=$R/gpurun_out/$O; mkdir -p $OUT
+O=r05d; OUT=$R/gpurun_out/$O; mkdir -p $OUT
 cd $R
-sha256sum raytracer-cuda_amd/csrc/crt_hip.hip raytracer-cuda_amd/lib/libcrt_hip.so > $OUT/sha.txt
-timeout -k 10 600 python3 -u -m pytest tests/test_gpu_rebuilt.py -m gpu -x -v --timeout 300 --timeout-method thread \
-    -k "tail_mode or wave_drain or persistent_queue or shipped" > $OUT/pytest_tail.log 2>&1
-S="t0:tail=0 t2:tail=2 t4:tail=4 t8:tail=8 t16:tail=16"
-timeout -k 10 300 python3 tools/schedule_sweep.py --width 1280 --height 720 --spp 256 --world 1 --reps 4 --set $S > $OUT/sweep_B.jsonl
-timeout -k 10 300 python3 tools/schedule_sweep.py --world 8 --reps 4 --set $S > $OUT/sweep_N8.jsonl
-timeout -k 10 600 python3 tools/schedule_sweep.py --world 1 --reps 3 --set t0:tail=0 t4:tail=4 t8:tail=8 > $OUT/sweep_C.jsonl
-for f in B N8 C; do python3 -c "
-import json
-for d in map(json.loads, open('$OUT/sweep_$f.jsonl')): print('$f', d['name'], d['main_median_ms'], d['main_ms_reps'], d.get('rays'))"; done
+B="CRT_SKIP_ABI_CHECK=1 CRT_HIP_LIB=$R/raytracer-cuda_amd/lib_exp/base/libcrt_hip.so CRT_HOST_LIB=$R/raytracer-cuda_amd/lib_exp/base/libcrt_host.so"
+sha256sum raytracer-cuda_amd/csrc/crt_hip.hip raytracer-cuda_amd/lib/libcrt_hip.so raytracer-cuda_amd/lib_exp/base/libcrt_hip.so > $OUT/sha.txt
+timeout -k 10 300 python3 tools/frame_hash.py --big > $OUT/hash_A.txt 2>&1
+env $B timeout -k 10 300 python3 tools/frame_hash.py --big > $OUT/hash_base.txt 2>&1
+cmp $OUT/hash_A.txt $OUT/hash_base.txt && echo "hashes identical" | tee $OUT/hash_cmp.txt
+BN="--no-cpu-baseline --no-count --no-parity"
+for i in 1 2 3; do
+  timeout -k 10 300 python3 bench.py $BN > $OUT/C_A_$i.log 2>&1
+  env $B timeout -k 10 300 python3 bench.py $BN > $OUT/C_base_$i.log 2>&1
+  timeout -k 10 300 python3 bench.py $BN --width 1280 --height 720 --spp 256 --steps 5 > $OUT/B_A_$i.log 2>&1
+  env $B timeout -k 10 300 python3 bench.py $BN --width 1280 --height 720 --spp 256 --steps 5 > $OUT/B_base_$i.log 2>&1
+  timeout -k 10 300 python3 bench.py $BN --scene cornell_1m --spp 512 > $OUT/E_A_$i.log 2>&1
+  env $B timeout -k 10 300 python3 bench.py $BN --scene cornell_1m --spp 512 > $OUT/E_base_$i.log 2>&1
+done
+for f in $OUT/*_[0-9].log; do echo "$(basename $f) $(tail -1 $f | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["render_phases_ms_avg"]["main_kernel_ms"], d["value"])')"; done | sort
 echo job done
