@@ -292,6 +292,10 @@ int  crt_renderer_set_wave_drain(crt_renderer* r, int sixty_fourths);
  * Every pixel is traced by one lane at a time, samples in order, from its own RNG stream: results never depend on it.
  * Defaults 8, 44, -1. */
 int  crt_renderer_set_consolidation(crt_renderer* r, int lanes, int threshold, int blocks);
+/* Variant 11: besides the trailing consumers, one consumer workgroup per `every` workgroups (every - 1 tiles, then a
+ * consumer; 0 = none; default 9) that takes queued paths only when `min_paths` (1..64, default 32) are ready and never
+ * waits, so handed-off paths are finished while tiles still run.  Results never depend on it. */
+int  crt_renderer_set_consolidation_interleave(crt_renderer* r, int every, int min_paths);
 /* Variant 11's queue after the last render: entries reserved, taken, tile waves done, consumer spin-outs (must be 0). */
 int  crt_renderer_get_consolidation_stats(crt_renderer* r, uint32_t out[4]);
 /* Variant 8 with the cost probe: 1 = the blocks that share an XCD (block index mod 8, MI355X's round-robin dispatch)

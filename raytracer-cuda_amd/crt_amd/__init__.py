@@ -323,6 +323,11 @@ class Renderer:
         check(_lib.hip().crt_renderer_set_consolidation(self.h, int(lanes), int(threshold), int(blocks)),
               "set_consolidation")
 
+    def set_consolidation_interleave(self, every: int = 9, min_paths: int = 32):
+        """Variant 11's interleaved consumers (crt_renderer_set_consolidation_interleave).  Results never depend on it."""
+        check(_lib.hip().crt_renderer_set_consolidation_interleave(self.h, int(every), int(min_paths)),
+              "set_consolidation_interleave")
+
     def consolidation_stats(self) -> dict:
         """Variant 11's queue after the last render (crt_renderer_get_consolidation_stats)."""
         a = (C.c_uint32 * 4)()

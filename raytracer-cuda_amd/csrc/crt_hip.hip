@@ -88,6 +88,7 @@ struct RenderParams {
     // ends; the trailing cons_blocks workgroups (blockIdx >= cons_tiles) take the queued paths 64 at a time and finish
     // them.  Every pixel is still traced by one lane at a time, samples in order, from its own RNG stream.
     int cons_lanes, cons_tiles, cons_cap, cons_threshold;
+    int cons_every, cons_inter, cons_min;  // interleaved consumers: one per cons_every workgroups for cons_inter groups
     uint32_t* __restrict__ cons_ctl;      // [0] entries reserved, [1] entries taken, [2] tile waves done, [3] spin-outs
     uint32_t* __restrict__ cons_flag;     // per entry: 1 once its record is written
     float4* __restrict__ cons_rec;        // per entry: 6 float4 (CONS_REC_WORDS words)
@@ -1448,9 +1449,24 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: LDS bases stay scalar
     int x, y;
     // variant 11: the trailing workgroups are consumers of the straggler queue (their lanes' pixels come from it)
-    const bool consumer = CONS && (int)blockIdx.x >= P.cons_tiles;
+    // With cons_every = M > 0 the first cons_inter groups of M workgroups are M - 1 tiles and one consumer that takes
+    // queued paths only when at least cons_min are ready and never waits; after them come the remaining tiles, then the
+    // trailing consumers, which wait for the queue to fill or to be final.  tile_pos: the workgroup's position in the
+    // cost order.
+    int tile_pos = (int)blockIdx.x;
+    bool consumer = false, sweeper = false;
+    if constexpr (CONS) {
+        const int b = (int)blockIdx.x, M = P.cons_every, inter = M > 0 ? P.cons_inter : 0;
+        if (b < inter * M) {
+            consumer = b % M == M - 1;
+            tile_pos = (b / M) * (M - 1) + b % M;
+        } else {
+            tile_pos = b - inter;
+            consumer = sweeper = tile_pos >= P.cons_tiles;
+        }
+    }
     if (TILES) {                               // workgroup b renders 8x8 tile order[b]
-        const uint32_t t = consumer ? 0u : P.order ? P.order[blockIdx.x] : blockIdx.x;
+        const uint32_t t = consumer ? 0u : P.order ? P.order[tile_pos] : (uint32_t)tile_pos;
         x = (int)(t % (uint32_t)P.tiles_x) * 8 + (lane & 7);
         y = (int)(t / (uint32_t)P.tiles_x) * 8 + (lane >> 3);
     } else {
@@ -1629,7 +1645,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         // variant 8: the most expensive tiles of the cost order bound the frame when it has few tiles per wave slot
         // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
         const int regen_t = consumer ? P.cons_threshold
-                                     : (TILED && (int)blockIdx.x < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
+                                     : (TILED && tile_pos < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
         bool first_pass = true;    // uniform
         bool dump_ok = CONS && !consumer && P.cons_lanes > 0;   // uniform: this tile wave may still hand off stragglers
 #ifdef CRT_PROFILE_LIVE
@@ -1655,7 +1671,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         pop = __builtin_amdgcn_readfirstlane(pop);
                         const uint32_t avail = resv - pop;
                         const bool all_done = (int)done >= P.cons_tiles;
-                        if (avail >= 64u || (all_done && avail > 0u)) {
+                        if (!sweeper && avail < (uint32_t)P.cons_min) break;   // an interleaved consumer never waits
+                        if (avail >= 64u || (all_done && avail > 0u) || (!sweeper && avail > 0u)) {
                             const uint32_t take = min(avail, 64u);
                             uint32_t got = 0;
                             if (lane == 0) got = atomicCAS(&P.cons_ctl[1], pop, pop + take);
@@ -2954,6 +2971,8 @@ struct crt_renderer {
     int cons_lanes = 8;            // variant 11: a tile wave hands off its stragglers at <= cons_lanes live lanes
     int cons_threshold = 44;       // variant 11: regeneration threshold of the consumer waves
     int cons_blocks = -1;          // variant 11: consumer workgroups after the tiles (-1 = 2 per CU)
+    int cons_every = 9;            // variant 11: one interleaved consumer per cons_every workgroups (0 = none)
+    int cons_min = 32;             // variant 11: an interleaved consumer starts only with this many paths queued
     uint32_t* d_cons_ctl = nullptr;
     uint32_t* d_cons_flag = nullptr;
     float4* d_cons_rec = nullptr;
@@ -3639,7 +3658,10 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             P.cons_flag = R->d_cons_flag;
             P.cons_rec = R->d_cons_rec;
             if (!R->n_cus) HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
-            tgrid.x += (unsigned)(R->cons_blocks >= 0 ? R->cons_blocks : 2 * R->n_cus);
+            P.cons_every = R->cons_every >= 2 ? R->cons_every : 0;
+            P.cons_inter = P.cons_every ? (int)tgrid.x / (P.cons_every - 1) : 0;
+            P.cons_min = R->cons_min;
+            tgrid.x += (unsigned)P.cons_inter + (unsigned)(R->cons_blocks >= 0 ? R->cons_blocks : 2 * R->n_cus);
         }
         HIP_TRY(hipEventRecord(R->ev_main, st));
         if (wv == 11) {
@@ -4061,6 +4083,14 @@ int crt_renderer_set_consolidation(crt_renderer* R, int lanes, int threshold, in
     R->cons_lanes = lanes;
     R->cons_threshold = threshold;
     R->cons_blocks = blocks;
+    return CRT_OK;
+}
+
+int crt_renderer_set_consolidation_interleave(crt_renderer* R, int every, int min_paths) {
+    if (!R || every < 0 || every == 1 || every > 4096 || min_paths < 1 || min_paths > 64)
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "consolidation interleave: every 0 or 2..4096, min_paths 1..64");
+    R->cons_every = every;
+    R->cons_min = min_paths;
     return CRT_OK;
 }
 

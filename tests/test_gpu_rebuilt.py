@@ -448,14 +448,17 @@ def test_straggler_consolidation_is_bit_identical(rebuilt, config):
     lanes hands their paths to a device queue and ends; consumer workgroups finish them 64 at a time.  Each pixel is still
     traced by one lane at a time, samples in order, on its own RNG stream, so frames, RNG state, the ray count and the
     counting kernel's box / triangle / sphere tests and paths equal variant 8's; every queued path is taken, no consumer
-    gave up waiting; ragged sizes, occupancy 6 and 7, and the SBVH tree included."""
+    gave up waiting; with and without interleaved consumers, ragged sizes, occupancy 6 and 7, and the SBVH tree."""
     dev = rebuilt["cornell_bunny", config]
     for w, h, spp in ((640, 360, 64), (100, 37, 70), (2560, 1440, 64)):
         out = []
-        for variant, lanes, thr in ((8, 8, 44), (11, 8, 44), (11, 32, 16), (11, 63, 44)):
+        # (variant, hand-off lanes, consumer threshold, one interleaved consumer per `every` workgroups, its minimum batch)
+        for variant, lanes, thr, every, mn in ((8, 8, 44, 9, 32), (11, 8, 44, 9, 32), (11, 32, 16, 3, 1),
+                                               (11, 63, 44, 0, 32)):
             r = crt_amd.Renderer(w, h)
             r.set_kernel_variant(variant)
             r.set_consolidation(lanes, thr, -1)
+            r.set_consolidation_interleave(every, mn)
             r.set_camera(crt_amd.camera(spp))
             r.init_rand(41)
             r.render(dev, spp, 20)

@@ -38,7 +38,7 @@ for f in $OUT/*_[0-9].log; do echo "$(basename $f) $(tail -1 $f | python3 -c 'im
 # variant 11 (straggler consolidation): bit identity, then variant 8 vs 11 at hand-off lanes 4/8/16 interleaved
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_rebuilt.py -m gpu -x -v --timeout 300 --timeout-method thread \
     -k "consolidation or wave_drain" > $OUT/pytest_v11.log 2>&1
-S="v8:v=8 c4:v=11,cl=4 c8:v=11,cl=8 c16:v=11,cl=16 c8t16:v=11,cl=8,ct=16"
+S="v8:v=8 c8:v=11,cl=8 c16:v=11,cl=16 c8e0:v=11,cl=8,ce=0 c8e5:v=11,cl=8,ce=5,cm=16 c16t16:v=11,cl=16,ct=16"
 timeout -k 10 300 python3 tools/schedule_sweep.py --width 1280 --height 720 --spp 256 --world 1 --reps 3 --set $S > $OUT/v11_B.jsonl
 timeout -k 10 300 python3 tools/schedule_sweep.py --world 8 --reps 3 --set $S > $OUT/v11_N8.jsonl
 timeout -k 10 600 python3 tools/schedule_sweep.py --world 1 --reps 2 --set $S > $OUT/v11_C.jsonl

@@ -6,7 +6,8 @@ time (best and median), the render with the probe and tile sort, and the rays.  
 `name:key=value,key=value` with keys crit (critical tiles, -1 = auto), lanes (their threshold), T (regeneration
 threshold), occ (waves per SIMD, 0 = auto), stride (probe stride, 0 = auto), probe (probe spp, -1 = auto), wd (the wave
 drain in 64ths, crt_renderer_set_wave_drain), v (kernel variant, -1 = automatic; 11 = variant 8 with straggler
-consolidation), cl / ct / cb (variant 11's hand-off lanes, consumer threshold, consumer blocks).  Results
+consolidation), cl / ct / cb / ce / cm (variant 11's hand-off lanes, consumer threshold, trailing consumer blocks,
+one interleaved consumer per ce workgroups (0 = none), their minimum batch).  Results
 never depend on them; the ray count is printed so that a setting that changed the work would show.
 
     python tools/schedule_sweep.py --world 8 --set base: crit0:crit=0 crit2k:crit=2048 T40:T=40 occ6:occ=6
@@ -35,7 +36,7 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--set", nargs="+", default=["base:"])
 a = ap.parse_args()
 
-DEFAULT = {"crit": -1, "lanes": 16, "T": 44, "occ": 0, "stride": 0, "probe": -1, "wd": 48, "v": -1, "cl": 8, "ct": 44, "cb": -1}
+DEFAULT = {"crit": -1, "lanes": 16, "T": 44, "occ": 0, "stride": 0, "probe": -1, "wd": 48, "v": -1, "cl": 8, "ct": 44, "cb": -1, "ce": 9, "cm": 32}
 settings = []
 for s in a.set:
     name, _, kv = s.partition(":")
@@ -64,6 +65,7 @@ def run(d: dict) -> dict:
     r.set_wave_drain(d["wd"])
     r.set_kernel_variant(d["v"])
     r.set_consolidation(d["cl"], d["ct"], d["cb"])
+    r.set_consolidation_interleave(d["ce"], d["cm"])
     r.init_rand(41, base)
     r.render(sc, spp, a.bounces)
     r.synchronize()
