@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CRT_ABI_VERSION 4
+#define CRT_ABI_VERSION 3
 
 enum crt_status {
     CRT_OK = 0,
@@ -285,19 +285,6 @@ int  crt_renderer_set_drain_threshold(crt_renderer* r, int lanes);
  * runs when `sixty_fourths`/64 of those live lanes are parked (1..64; 64 = only when all of them are; default 48), so
  * the wave's last pixels wait less for each other's paths.  Results never depend on it. */
 int  crt_renderer_set_wave_drain(crt_renderer* r, int sixty_fourths);
-/* Variant 11 = variant 8 + straggler consolidation (select it with crt_renderer_set_kernel_variant(r, 11)): a tile wave
- * whose lanes with samples left drop to `lanes` (1..63; 0 = never) waits until all of them are parked, shades them and
- * hands each path (its next ray set up) to a device queue, then ends; `blocks` consumer workgroups launched after the
- * tiles (-1 = 2 per CU) take the queued paths 64 at a time and finish them with regeneration threshold `threshold`.
- * Every pixel is traced by one lane at a time, samples in order, from its own RNG stream: results never depend on it.
- * Defaults 8, 44, -1. */
-int  crt_renderer_set_consolidation(crt_renderer* r, int lanes, int threshold, int blocks);
-/* Variant 11: besides the trailing consumers, one consumer workgroup per `every` workgroups (every - 1 tiles, then a
- * consumer; 0 = none; default 9) that takes queued paths only when `min_paths` (1..64, default 32) are ready and never
- * waits, so handed-off paths are finished while tiles still run.  Results never depend on it. */
-int  crt_renderer_set_consolidation_interleave(crt_renderer* r, int every, int min_paths);
-/* Variant 11's queue after the last render: entries reserved, taken, tile waves done, consumer spin-outs (must be 0). */
-int  crt_renderer_get_consolidation_stats(crt_renderer* r, uint32_t out[4]);
 /* Variant 8 with the cost probe: 1 = the blocks that share an XCD (block index mod 8, MI355X's round-robin dispatch)
  * render one screen strip of equal probe cost, most expensive tile first, so each XCD's L2 holds its strip's geometry;
  * 0 = one global cost order (default).  Ignored with pixel sharding.  Results never depend on it. */

@@ -318,22 +318,6 @@ class Renderer:
         """Variant 7: regeneration threshold once the pixel queue is empty, 0 = unchanged (crt_renderer_set_drain_threshold)."""
         check(_lib.hip().crt_renderer_set_drain_threshold(self.h, int(lanes)), "set_drain_threshold")
 
-    def set_consolidation(self, lanes: int = 8, threshold: int = 44, blocks: int = -1):
-        """Variant 11's straggler consolidation (crt_renderer_set_consolidation).  Results never depend on it."""
-        check(_lib.hip().crt_renderer_set_consolidation(self.h, int(lanes), int(threshold), int(blocks)),
-              "set_consolidation")
-
-    def set_consolidation_interleave(self, every: int = 9, min_paths: int = 32):
-        """Variant 11's interleaved consumers (crt_renderer_set_consolidation_interleave).  Results never depend on it."""
-        check(_lib.hip().crt_renderer_set_consolidation_interleave(self.h, int(every), int(min_paths)),
-              "set_consolidation_interleave")
-
-    def consolidation_stats(self) -> dict:
-        """Variant 11's queue after the last render (crt_renderer_get_consolidation_stats)."""
-        a = (C.c_uint32 * 4)()
-        check(_lib.hip().crt_renderer_get_consolidation_stats(self.h, a), "get_consolidation_stats")
-        return {"reserved": int(a[0]), "taken": int(a[1]), "tile_waves_done": int(a[2]), "spin_outs": int(a[3])}
-
     def set_wave_drain(self, sixty_fourths: int):
         """Variants 4/8: a draining wave passes at sixty_fourths/64 of its live lanes (crt_renderer_set_wave_drain)."""
         check(_lib.hip().crt_renderer_set_wave_drain(self.h, int(sixty_fourths)), "set_wave_drain")

@@ -83,15 +83,6 @@ struct RenderParams {
     int drain_threshold;                  // variant 7: the threshold once the pixel queue is empty
     int wave_drain;                       // variants 4/8: sixty-fourths of the live lanes a draining wave passes at
     int top_levels;                       // 4-wide variants: a new ray's first node steps taken from LDS (<= CRT_TOP_LEVELS)
-    // variant 11 = variant 8 + straggler consolidation (crt_renderer_set_consolidation): a tile wave whose live lanes
-    // drop to cons_lanes parks them all, then hands each one's path state (its next ray ready) to a device queue and
-    // ends; the trailing cons_blocks workgroups (blockIdx >= cons_tiles) take the queued paths 64 at a time and finish
-    // them.  Every pixel is still traced by one lane at a time, samples in order, from its own RNG stream.
-    int cons_lanes, cons_tiles, cons_cap, cons_threshold;
-    int cons_every, cons_inter, cons_min;  // interleaved consumers: one per cons_every workgroups for cons_inter groups
-    uint32_t* __restrict__ cons_ctl;      // [0] entries reserved, [1] entries taken, [2] tile waves done, [3] spin-outs
-    uint32_t* __restrict__ cons_flag;     // per entry: 1 once its record is written
-    float4* __restrict__ cons_rec;        // per entry: 6 float4 (CONS_REC_WORDS words)
 };
 
 #ifdef CRT_PROFILE_LIVE
@@ -984,9 +975,7 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
     }
 }
 
-// FRESH: the lane's LDS key address from the lane id at the point of use (lane_fresh), for kernels whose allocator would
-// otherwise keep &L.key[lane] in a scratch slot and reload it on every leaf step (variant 11)
-template <bool COUNT, bool FRESH = false>
+template <bool COUNT>
 __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
                                                float& closest, int& hit, TraceCounts& cnt, WaveLdsWide& L,
                                                uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix) {
@@ -1023,7 +1012,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         // the loop and spills it (a scratch reload and a vmcnt(0) wait on every leaf step)
         uint32_t ones;
         __asm__ volatile("v_mov_b32 %0, -1" : "=v"(ones));
-        L.key[FRESH ? lane_fresh() : lane] = ((unsigned long long)ones << 32) | ones;
+        L.key[lane] = ((unsigned long long)ones << 32) | ones;
     }
     uint32_t carry = 0;   // owner + 1 of the last pair of the previous round
     for (int base = 0; base < total; base += 64) {
@@ -1071,7 +1060,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         wave_sync();
     }
     {
-        const unsigned long long kk = L.key[FRESH ? lane_fresh() : lane];
+        const unsigned long long kk = L.key[lane];
         const float t = __uint_as_float((unsigned)(kk >> 32));
         const int rank = (int)(0xffffffffu - (unsigned)kk);
         if (leaf_n > 0 && kk != ~0ull && better(t, rank, closest, hit)) {
@@ -1150,17 +1139,6 @@ __device__ __forceinline__ void top_steps(const RenderParams& P, const float4* t
         return;
     const int m = node - __float_as_int(top[6].x);   // node is an internal child of the root: slot m < 4
     if ((unsigned)m < 4u) top_step4<COUNT>(P, top + 8 * (1 + m), o, inv, rows, node, sp, cnt, stk, pix, n_pix);
-}
-
-// Pixel coordinates of pixel index p < 2^23 for a frame of width w: q = trunc(p * RN(1/w)) is within one of p / w, one
-// correction each way makes it exact (variant 11, which keeps only the index per lane).
-__device__ __forceinline__ void pix_xy(int p, int w, float rcp_w, int& x, int& y) {
-    int q = (int)((float)p * rcp_w);
-    int r = p - q * w;
-    if (r < 0) { --q; r += w; }
-    if (r >= w) { ++q; r -= w; }
-    x = r;
-    y = q;
 }
 
 // Per-lane path state of one pixel (rayColor's locals, CUDAKernels.h:102-145, plus the sample loop).
@@ -1383,14 +1361,7 @@ __device__ unsigned long long g_wave_prof[2 * 4 * 65536];
 
 // Waves per workgroup: 4 (16x16 pixels), or 1 for variant 8 (one 8x8 tile per workgroup, so a finished wave frees
 // its slot at once instead of holding it until its three siblings end).
-template <int VARIANT> struct KernelShape {
-    static constexpr int waves = VARIANT == 8 || VARIANT == 10 || VARIANT == 11 ? 1 : 4;
-};
-
-// Variant 11's queue record of one straggler path (after its parked pass: the next ray is set up in o, d): pixel, XORWOW
-// state, the pixel's running sum, o, d, throughput, samples left, bounce.
-constexpr int CONS_REC_F4 = 6;
-constexpr uint32_t CONS_SPIN_LIMIT = 1u << 24;   // polls before a waiting consumer gives up (error bit 8, no hang)
+template <int VARIANT> struct KernelShape { static constexpr int waves = VARIANT == 8 || VARIANT == 10 ? 1 : 4; };
 
 template <bool COUNT, int VARIANT, int MINW>
 __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_render_kernel(RenderParams P) {
@@ -1400,8 +1371,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     constexpr int WGW = KernelShape<VARIANT>::waves;
     // variant 4: 16 LDS stack entries per lane at 5 waves/SIMD; 12 at 6+ so 6 workgroups fit the 160 KiB
     constexpr bool PERSIST = VARIANT == 7;
-    constexpr bool CONS = VARIANT == 11;    // variant 8 + straggler consolidation
-    constexpr bool TILED = VARIANT == 8 || CONS;    // variant 4 with one wave per workgroup and a tile order
+    constexpr bool TILED = VARIANT == 8;    // variant 4 with one wave per workgroup and a tile order
     constexpr bool TILES = TILED || VARIANT == 10;   // one 8x8 tile per one-wave workgroup (variant 10: variant 3's program)
     constexpr bool WIDE = VARIANT == 4 || PERSIST || TILED;
     using Lds = std::conditional_t<WIDE, WaveLdsWide, WaveLds>;
@@ -1446,25 +1416,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: LDS bases stay scalar
     int x, y;
-    // variant 11: the trailing workgroups are consumers of the straggler queue (their lanes' pixels come from it)
-    // With cons_every = M > 0 the first cons_inter groups of M workgroups are M - 1 tiles and one consumer that takes
-    // queued paths only when at least cons_min are ready and never waits; after them come the remaining tiles, then the
-    // trailing consumers, which wait for the queue to fill or to be final.  tile_pos: the workgroup's position in the
-    // cost order.
-    int tile_pos = (int)blockIdx.x;
-    bool consumer = false, sweeper = false;
-    if constexpr (CONS) {
-        const int b = (int)blockIdx.x, M = P.cons_every, inter = M > 0 ? P.cons_inter : 0;
-        if (b < inter * M) {
-            consumer = b % M == M - 1;
-            tile_pos = (b / M) * (M - 1) + b % M;
-        } else {
-            tile_pos = b - inter;
-            consumer = sweeper = tile_pos >= P.cons_tiles;
-        }
-    }
     if (TILES) {                               // workgroup b renders 8x8 tile order[b]
-        const uint32_t t = consumer ? 0u : P.order ? P.order[(uint32_t)tile_pos] : (uint32_t)tile_pos;
+        const uint32_t t = P.order ? P.order[blockIdx.x] : blockIdx.x;
         x = (int)(t % (uint32_t)P.tiles_x) * 8 + (lane & 7);
         y = (int)(t / (uint32_t)P.tiles_x) * 8 + (lane >> 3);
     } else {
@@ -1475,12 +1428,8 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             y *= P.probe_stride;
         }
     }
-    const bool valid = !consumer && x < P.width && y < P.height;
+    const bool valid = x < P.width && y < P.height;
     const int pix = valid ? y * P.width + x : 0;
-    // variant 11 keeps ONE per-lane pixel value, -1 = none (an invalid lane, a consumer lane without a path, a path handed
-    // to the queue): x and y are derived from it where next_ray needs them (pix_xy), so the tile waves' and the
-    // consumers' lanes carry no extra registers through the loop
-    int pix_c = CONS ? (valid ? pix : -1) : 0;
 
     PathState S;
     S.s = Rng{0, 0, 0, 0, 0, 0};
@@ -1642,231 +1591,84 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         if (TILED && lane == 0) L.rays = 0;
         // variant 8: the most expensive tiles of the cost order bound the frame when it has few tiles per wave slot
         // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
-        const int regen_t = consumer ? P.cons_threshold
-                                     : (TILED && tile_pos < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
+        const int regen_t = (TILED && (int)blockIdx.x < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
         bool first_pass = true;    // uniform
-        bool dump_ok = CONS && !consumer && P.cons_lanes > 0;   // uniform: this tile wave may still hand off stragglers
 #ifdef CRT_PROFILE_LIVE
         uint64_t lh0 = 0, lh1 = 0, lh2 = 0, lh3 = 0, lh4 = 0, lh5 = 0, lh6 = 0, lh7 = 0, lh8 = 0;
         uint64_t lt_prev = shader_clock();
         int lb_prev = 8;
 #endif
-        for (;;) {   // variant 11 consumers: one iteration per batch of queued stragglers; every other wave: once
-            if constexpr (CONS) {
-                if (consumer) {
-                    // take up to 64 queued paths: wait until 64 are reserved, or every tile wave has ended (then the
-                    // queue is final), and claim a range by CAS; a lane waits for its entry's record to be written
-                    uint32_t start = 0, n = 0, spins = 0;
-                    for (;;) {
-                        // read order matters: `taken` only ever advances to a `reserved` value some consumer saw, so reading
-                        // taken, then done, then reserved gives taken <= reserved, and reserved is final when done says so
-                        uint32_t done = 0, resv = 0, pop = 0;
-                        if (lane == 0) {
-                            pop = __hip_atomic_load(&P.cons_ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                            done = __hip_atomic_load(&P.cons_ctl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                            resv = __hip_atomic_load(&P.cons_ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                        done = __builtin_amdgcn_readfirstlane(done);
-                        resv = __builtin_amdgcn_readfirstlane(resv);
-                        pop = __builtin_amdgcn_readfirstlane(pop);
-                        const uint32_t avail = resv > pop ? resv - pop : 0u;
-                        const bool all_done = (int)done >= P.cons_tiles;
-                        if (!sweeper && avail < (uint32_t)P.cons_min) break;   // an interleaved consumer never waits
-                        if (avail >= 64u || (all_done && avail > 0u) || (!sweeper && avail > 0u)) {
-                            const uint32_t take = min(avail, 64u);
-                            uint32_t got = 0;
-                            if (lane == 0) got = atomicCAS(&P.cons_ctl[1], pop, pop + take);
-                            if (__builtin_amdgcn_readfirstlane(got) == pop) { start = pop; n = take; break; }
-                            continue;
-                        }
-                        if (all_done || ++spins >= CONS_SPIN_LIMIT) {
-                            if (!all_done && lane == 0) atomicAdd(&P.cons_ctl[3], 1u);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(8);
+        for (;;) {
+            const uint64_t parked_mask = live_mask & wave_ballot(node < 0);
+            const int n_parked = __popcll(parked_mask);
+            const int n_live = __popcll(live_mask);
+#ifdef CRT_PROFILE_LIVE
+            if (TILED) {
+                const uint64_t lt = shader_clock(), dt = lt - lt_prev;
+                lt_prev = lt;
+                lh0 += lb_prev == 0 ? dt : 0; lh1 += lb_prev == 1 ? dt : 0; lh2 += lb_prev == 2 ? dt : 0;
+                lh3 += lb_prev == 3 ? dt : 0; lh4 += lb_prev == 4 ? dt : 0; lh5 += lb_prev == 5 ? dt : 0;
+                lh6 += lb_prev == 6 ? dt : 0; lh7 += lb_prev == 7 ? dt : 0; lh8 += lb_prev == 8 ? dt : 0;
+                lb_prev = n_live >> 3;
+                if (n_live == 0 && lane == 0) {
+                    atomicAdd(&g_live_hist[0], lh0); atomicAdd(&g_live_hist[1], lh1); atomicAdd(&g_live_hist[2], lh2);
+                    atomicAdd(&g_live_hist[3], lh3); atomicAdd(&g_live_hist[4], lh4); atomicAdd(&g_live_hist[5], lh5);
+                    atomicAdd(&g_live_hist[6], lh6); atomicAdd(&g_live_hist[7], lh7); atomicAdd(&g_live_hist[8], lh8);
+                }
+            }
+#endif
+            if (n_live == 0) break;
+            const uint64_t c0 = COUNT ? shader_clock() : 0;
+            // once fewer than regen_t lanes still have samples, waiting for every live lane to park before a pass makes
+            // each of them wait for the slowest path of the others at every bounce; a pass at wave_drain/64 of them
+            // (crt_renderer_set_wave_drain; 64 = all) shortens the wave's own drain (profiles/r04n)
+            const bool drain_pass = n_live < regen_t && n_parked * 64 >= n_live * P.wave_drain;
+            if (n_parked >= regen_t || n_parked == n_live || drain_pass) {
+                if (COUNT) cnt.passes++;
+                if (__builtin_amdgcn_inverse_ballot_w64(parked_mask)) {
+                    const uint64_t s0 = COUNT ? shader_clock() : 0;
+                    // (loading the shading record before this sphere test, to overlap its latency, measured +0.7 %:
+                    // profiles/r01ar)
+                    // after the first pass every parked lane holds a result (parked_mask is within live_mask, which is
+                    // the lanes with a ray): a uniform test instead of a divergent branch on has_result (-0.38 %,
+                    // profiles/r02av)
+                    if (!first_pass) {
+                        finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, s0);
                     }
-                    if (n == 0) break;   // the queue is empty and final
-                    bool mine = (uint32_t)lane < n && start + (uint32_t)lane < (uint32_t)P.cons_cap;
-                    if (mine) {
-                        const uint32_t idx = start + (uint32_t)lane;
-                        uint32_t w = 0;
-                        while (__hip_atomic_load(&P.cons_flag[idx], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
-                               ++w < CONS_SPIN_LIMIT)
-                            __builtin_amdgcn_s_sleep(2);
-                        if (w >= CONS_SPIN_LIMIT) {   // never written (a bug): count it and leave the lane idle
-                            atomicAdd(&P.cons_ctl[3], 1u);
-                            mine = false;
-                        }
+                    const uint64_t s1 = COUNT ? shader_clock() : 0;
+                    const bool live = next_ray(S, C, x, y, P.max_bounces);
+                    if (COUNT) {
+                        const uint64_t s2 = shader_clock();
+                        cnt.cyc_shade += s1 - s0;
+                        cnt.cyc_next += s2 - s1;
                     }
-                    if (mine) {
-                        const uint32_t idx = start + (uint32_t)lane;
-                        const float4* rec = P.cons_rec + (size_t)idx * CONS_REC_F4;
-                        const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3], q4 = rec[4], q5 = rec[5];
-                        pix_c = __float_as_int(q0.x);
-                        S.s = Rng{__float_as_uint(q0.y), __float_as_uint(q0.z), __float_as_uint(q0.w), __float_as_uint(q1.x),
-                                  __float_as_uint(q1.y), __float_as_uint(q1.z)};
-                        S.pixel = v3(q1.w, q2.x, q2.y);
-                        S.o = v3(q2.z, q2.w, q3.x);
-                        S.d = v3(q3.y, q3.z, q3.w);
-                        S.thr = v3(q4.x, q4.y, q4.z);
-                        S.remaining = __float_as_int(q4.w);
-                        S.bounce = __float_as_int(q5.x);
-                        S.need_new = false;
-                    }
-                    // each taken path has its next ray ready (it was parked and shaded): start it as a pass would
-                    has_result = mine;
-                    if (mine) {
+                    has_result = false;
+                    if (live) {
+                        if (!TILED) ++S.rays;
+                        has_result = true;
                         node = 0;
                         sp = 0;
                         closest = INF;
                         hit = -1;
+                        // exact 1/d: the per-ray spheres' reference box tests need it (the padded traversal
+                        // would do with rcp)
                         inv = recip3_exact(S.d);
-                        inv = box_inv(inv);
+                        inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
                         rows = ray_rows(inv);
                         if (COUNT) cnt.spheres += P.n_ray_spheres;
                         L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                         if (COUNT) cnt.trace_calls++;
-                        if (TOPN > 0) top_steps<COUNT, TOPN>(P, top_lds, S.o, inv, rows, node, sp, cnt, stk, (size_t)pix_c, n_pix);
+                        if (TOPN > 0) top_steps<COUNT, TOPN>(P, top_lds, S.o, inv, rows, node, sp, cnt, stk, (size_t)pix, n_pix);
                     }
-                    live_mask = wave_ballot(has_result);
-                    if (lane == 0) atomicAdd(&L.rays, (uint32_t)__popcll(live_mask));
-                    first_pass = false;
                 }
+                live_mask = wave_ballot(has_result);
+                first_pass = false;
+                // variant 8 counts the wave's rays in LDS (one VGPR less in the hot loop); (an LDS add without return
+                // instead of the read-modify-write measured +0.4 % on config C, profiles/r05e)
+                if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);
             }
-            for (;;) {
-                const uint64_t parked_mask = live_mask & wave_ballot(node < 0);
-                const int n_parked = __popcll(parked_mask);
-                const int n_live = __popcll(live_mask);
-#ifdef CRT_PROFILE_LIVE
-                if (TILED) {
-                    const uint64_t lt = shader_clock(), dt = lt - lt_prev;
-                    lt_prev = lt;
-                    lh0 += lb_prev == 0 ? dt : 0; lh1 += lb_prev == 1 ? dt : 0; lh2 += lb_prev == 2 ? dt : 0;
-                    lh3 += lb_prev == 3 ? dt : 0; lh4 += lb_prev == 4 ? dt : 0; lh5 += lb_prev == 5 ? dt : 0;
-                    lh6 += lb_prev == 6 ? dt : 0; lh7 += lb_prev == 7 ? dt : 0; lh8 += lb_prev == 8 ? dt : 0;
-                    lb_prev = n_live >> 3;
-                    if (n_live == 0 && lane == 0) {
-                        atomicAdd(&g_live_hist[0], lh0); atomicAdd(&g_live_hist[1], lh1); atomicAdd(&g_live_hist[2], lh2);
-                        atomicAdd(&g_live_hist[3], lh3); atomicAdd(&g_live_hist[4], lh4); atomicAdd(&g_live_hist[5], lh5);
-                        atomicAdd(&g_live_hist[6], lh6); atomicAdd(&g_live_hist[7], lh7); atomicAdd(&g_live_hist[8], lh8);
-                        lh0 = lh1 = lh2 = lh3 = lh4 = lh5 = lh6 = lh7 = lh8 = 0;
-                    }
-                }
-#endif
-                if (n_live == 0) break;
-                const uint64_t c0 = COUNT ? shader_clock() : 0;
-                // variant 11: a tile wave down to cons_lanes live lanes waits until all of them are parked, shades them
-                // and hands their next rays to the straggler queue instead of tracing them
-                const bool dumping = CONS && dump_ok && n_live <= P.cons_lanes;
-                // once fewer than regen_t lanes still have samples, waiting for every live lane to park before a pass
-                // makes each of them wait for the slowest path of the others at every bounce; a pass at wave_drain/64
-                // of them (crt_renderer_set_wave_drain; 64 = all) shortens the wave's own drain (profiles/r04n)
-                const bool drain_pass = !dumping && n_live < regen_t && n_parked * 64 >= n_live * P.wave_drain;
-                if ((!dumping && n_parked >= regen_t) || n_parked == n_live || drain_pass) {
-                    if (COUNT) cnt.passes++;
-                    bool qfull = false;
-                    if (__builtin_amdgcn_inverse_ballot_w64(parked_mask)) {
-                        const uint64_t s0 = COUNT ? shader_clock() : 0;
-                        // (loading the shading record before this sphere test, to overlap its latency, measured
-                        // +0.7 %: profiles/r01ar)
-                        // after the first pass every parked lane holds a result (parked_mask is within live_mask, which
-                        // is the lanes with a ray): a uniform test instead of a divergent branch on has_result (-0.38 %,
-                        // profiles/r02av)
-                        if (!first_pass) {
-                            finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, s0);
-                        }
-                        const uint64_t s1 = COUNT ? shader_clock() : 0;
-                        int rx = x, ry = y;
-                        if constexpr (CONS) pix_xy(pix_c, P.width, P.rcp_w, rx, ry);
-                        const bool live = next_ray(S, C, rx, ry, P.max_bounces);
-                        if (COUNT) {
-                            const uint64_t s2 = shader_clock();
-                            cnt.cyc_shade += s1 - s0;
-                            cnt.cyc_next += s2 - s1;
-                        }
-                        has_result = false;
-                        bool keep = live;
-                        if constexpr (CONS) {
-                            if (dumping) {
-                                // reserve one queue entry per path that goes on (all or none: the queue only ever holds
-                                // entries that will be written), write its record, then release its flag
-                                const uint64_t go = wave_ballot(live);
-                                const uint32_t cnt_go = (uint32_t)__popcll(go);
-                                uint32_t base = 0xffffffffu;
-                                if (lane_fresh() == (int)__builtin_ctzll(parked_mask)) {
-                                    uint32_t cur = __hip_atomic_load(&P.cons_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                    while (cur + cnt_go <= (uint32_t)P.cons_cap) {
-                                        const uint32_t seen = atomicCAS(&P.cons_ctl[0], cur, cur + cnt_go);
-                                        if (seen == cur) { base = cur; break; }
-                                        cur = seen;
-                                    }
-                                }
-                                base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)__builtin_ctzll(parked_mask));
-                                if (base != 0xffffffffu) {
-                                    if (live) {
-                                        const uint32_t idx = base + (uint32_t)__popcll(go & ((1ull << lane) - 1ull));
-                                        float4* rec = P.cons_rec + (size_t)idx * CONS_REC_F4;
-                                        rec[0] = make_float4(__int_as_float(pix_c), __uint_as_float(S.s.v0), __uint_as_float(S.s.v1),
-                                                             __uint_as_float(S.s.v2));
-                                        rec[1] = make_float4(__uint_as_float(S.s.v3), __uint_as_float(S.s.v4),
-                                                             __uint_as_float(S.s.d), S.pixel.x);
-                                        rec[2] = make_float4(S.pixel.y, S.pixel.z, S.o.x, S.o.y);
-                                        rec[3] = make_float4(S.o.z, S.d.x, S.d.y, S.d.z);
-                                        rec[4] = make_float4(S.thr.x, S.thr.y, S.thr.z, __int_as_float(S.remaining));
-                                        rec[5] = make_float4(__int_as_float(S.bounce), 0.f, 0.f, 0.f);
-                                        __hip_atomic_store(&P.cons_flag[idx], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                                        pix_c = -1;   // its pixel is now the consumer's to store
-                                        keep = false;
-                                    }
-                                } else {
-                                    qfull = true;   // the queue is full: this wave finishes its own lanes
-                                }
-                            }
-                        }
-                        if (keep) {
-                            if (!TILED) ++S.rays;
-                            has_result = true;
-                            node = 0;
-                            sp = 0;
-                            closest = INF;
-                            hit = -1;
-                            // exact 1/d: the per-ray spheres' reference box tests need it (the padded traversal
-                            // would do with rcp)
-                            inv = recip3_exact(S.d);
-                            inv = box_inv(inv);   // the traversal's 1/d (wide_boxes)
-                            rows = ray_rows(inv);
-                            if (COUNT) cnt.spheres += P.n_ray_spheres;
-                            L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
-                            if (COUNT) cnt.trace_calls++;
-                            if (TOPN > 0) top_steps<COUNT, TOPN>(P, top_lds, S.o, inv, rows, node, sp, cnt, stk,
-                                                                 (size_t)(CONS ? pix_c : pix), n_pix);
-                        }
-                    }
-                    live_mask = wave_ballot(has_result);
-                    first_pass = false;
-                    if (CONS && dumping && wave_ballot(qfull)) dump_ok = false;   // uniform (all lanes active here)
-                    // variant 8 counts the wave's rays in LDS (one VGPR less in the hot loop); (an LDS add without
-                    // return instead of the read-modify-write measured +0.4 % on config C, profiles/r05e)
-                    if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);
-                }
-                if (COUNT) cnt.cyc_regen += shader_clock() - c0;
-                traverse_step4<COUNT, CONS>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane,
-                                            (size_t)(CONS ? pix_c : pix), n_pix);
-            }
-            if constexpr (CONS) {
-                if (consumer) {   // the batch's paths are done: store their pixels (CUDAKernels.h:162-165)
-                    if (pix_c >= 0) {
-                        uint32_t* r = P.rng + 6 * (size_t)pix_c;
-                        r[0] = S.s.v0; r[1] = S.s.v1; r[2] = S.s.v2; r[3] = S.s.v3; r[4] = S.s.v4; r[5] = S.s.d;
-                        P.sum[3 * (size_t)pix_c] = S.pixel.x;
-                        P.sum[3 * (size_t)pix_c + 1] = S.pixel.y;
-                        P.sum[3 * (size_t)pix_c + 2] = S.pixel.z;
-                    }
-                    pix_c = -1;
-                    continue;
-                }
-            }
-            break;
+            if (COUNT) cnt.cyc_regen += shader_clock() - c0;
+            traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
         }
     } else if constexpr (VARIANT == 2 || VARIANT == 3 || VARIANT == 10) {
         constexpr bool PF = VARIANT == 3 || VARIANT == 10;
@@ -1932,18 +1734,12 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         if (valid) P.probe_cost[pix] = COUNT ? (16u * S.rays + cnt.boxes + 4u * cnt.tris) >> 3 : S.rays;
         return;
     }
-    if (CONS ? pix_c >= 0 : valid && !PERSIST) {
-        const size_t pw = (size_t)(CONS ? pix_c : pix);
-        uint32_t* r = P.rng + 6 * pw;
+    if (valid && !PERSIST) {
+        uint32_t* r = P.rng + 6 * (size_t)pix;
         r[0] = S.s.v0; r[1] = S.s.v1; r[2] = S.s.v2; r[3] = S.s.v3; r[4] = S.s.v4; r[5] = S.s.d;
-        P.sum[3 * pw] = S.pixel.x;
-        P.sum[3 * pw + 1] = S.pixel.y;
-        P.sum[3 * pw + 2] = S.pixel.z;
-    }
-    if constexpr (CONS) {
-        // a tile wave has written every record it reserved (each with its release flag): count it done, so the
-        // consumers know when the queue is final
-        if (!consumer && lane == 0) __hip_atomic_fetch_add(&P.cons_ctl[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        P.sum[3 * (size_t)pix] = S.pixel.x;
+        P.sum[3 * (size_t)pix + 1] = S.pixel.y;
+        P.sum[3 * (size_t)pix + 2] = S.pixel.z;
     }
     if constexpr (TILED) wave_rays = lds[0].rays;
     const uint64_t wr = TILED ? (uint64_t)wave_rays : wave_sum_u64(S.rays);
@@ -2975,15 +2771,6 @@ struct crt_renderer {
     int temporal = 0;              // variant 7: tiles ordered by the previous variant-7 frame's rays per pixel
     int drain_threshold = 0;       // variant 7: regeneration threshold once the pixel queue is empty (0 = unchanged)
     int wave_drain = 48;           // variants 4/8: draining waves pass at 48/64 of their live lanes (profiles/r04n)
-    int cons_lanes = 8;            // variant 11: a tile wave hands off its stragglers at <= cons_lanes live lanes
-    int cons_threshold = 44;       // variant 11: regeneration threshold of the consumer waves
-    int cons_blocks = -1;          // variant 11: consumer workgroups after the tiles (-1 = 2 per CU)
-    int cons_every = 9;            // variant 11: one interleaved consumer per cons_every workgroups (0 = none)
-    int cons_min = 32;             // variant 11: an interleaved consumer starts only with this many paths queued
-    uint32_t* d_cons_ctl = nullptr;
-    uint32_t* d_cons_flag = nullptr;
-    float4* d_cons_rec = nullptr;
-    size_t cons_cap = 0;
     uint32_t* d_pix_rays = nullptr;   // variant 7 with the temporal order: rays per pixel of the last frame
     uint32_t* d_tile_order = nullptr; // its tiles, most expensive first
     bool pix_rays_valid = false;
@@ -3363,9 +3150,6 @@ void crt_renderer_destroy(crt_renderer* R) {
     if (R->d_pix_rays) (void)hipFree(R->d_pix_rays);
     if (R->d_tile_order) (void)hipFree(R->d_tile_order);
     if (R->d_rng_cache) (void)hipFree(R->d_rng_cache);
-    if (R->d_cons_ctl) (void)hipFree(R->d_cons_ctl);
-    if (R->d_cons_flag) (void)hipFree(R->d_cons_flag);
-    if (R->d_cons_rec) (void)hipFree(R->d_cons_rec);
     for (auto& slot : R->ring)
         for (hipEvent_t& ev : slot)
             if (ev) (void)hipEventDestroy(ev);
@@ -3403,8 +3187,8 @@ int crt_renderer_init_rand(crt_renderer* R, unsigned long long seed, unsigned lo
 }
 
 int crt_renderer_set_kernel_variant(crt_renderer* R, int variant) {
-    if (!R || variant < -1 || variant > 11 || variant == 5 || variant == 6 || variant == 9)
-        return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant (-1 = automatic, 0-4, 7, 8, 10, 11)");
+    if (!R || variant < -1 || variant > 10 || variant == 5 || variant == 6 || variant == 9)
+        return set_error(CRT_ERR_INVALID_ARGUMENT, "bad kernel variant (-1 = automatic, 0-4, 7, 8, 10)");
     R->variant = variant;
     return CRT_OK;
 }
@@ -3540,7 +3324,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     // 8 (probe-ordered tiles, one wave per workgroup) when the render runs the cost probe, 7 (lanes refill from a
     // pixel queue) for short renders such as the 1-spp interactive frames
     int wv = R->variant;
-    if (S->width == 4 && wv != 4 && wv != 7 && wv != 8 && wv != 11) wv = probe_spp_for(R, spp) > 0 ? 8 : 7;
+    if (S->width == 4 && wv != 4 && wv != 7 && wv != 8) wv = probe_spp_for(R, spp) > 0 ? 8 : 7;
     // threaded scenes (the bit-exact reference BVH, rebuilt width 2): variants 0-3 and 10 when selected explicitly;
     // otherwise 10 (variant 3 over probe-ordered 8x8 tiles, one wave per workgroup; -17 %, profiles/r03s) when the
     // render runs the cost probe, else 3
@@ -3553,7 +3337,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     // variants run at 6, threaded scenes at 5.
     // Variants 10 and 3 (threaded, bit-exact) run at 6 (80 VGPRs; -8.0 % and -4.8 % against 5, profiles/r03am, r03as).
     int occ = R->min_waves ? R->min_waves : (S->width == 4 || tv == 10 || tv == 3 ? 6 : 5);
-    if (!R->min_waves && S->width == 4 && (wv == 8 || wv == 11 || R->tile_shards > 1)) {
+    if (!R->min_waves && S->width == 4 && (wv == 8 || R->tile_shards > 1)) {
         if (!R->n_cus) HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
         const size_t tiles = (size_t)((R->width + 7) / 8) * ((R->height + 7) / 8) / (size_t)std::max(1, R->tile_shards);
         if (tiles >= (size_t)4 * R->n_cus * 4 * 7) occ = 7;
@@ -3576,7 +3360,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         P.ovf = R->d_ovf;
     }
     if (R->tile_shards > 1) wv = 8;   // pixel sharding (checked above)
-    if (S->width == 4 && (wv == 8 || wv == 11)) {
+    if (S->width == 4 && wv == 8) {
         const size_t n_pix = (size_t)R->width * R->height;
         const int tiles_x = (R->width + 7) / 8, n_tiles = tiles_x * ((R->height + 7) / 8);
         if (!R->d_tile_key) {
@@ -3637,54 +3421,10 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             P.order = R->d_order;
         }
         if (P.crit_tiles > 0) P.crit_tiles = (P.crit_tiles + R->tile_shards - 1) / R->tile_shards;
-        dim3 tgrid((unsigned)((n_tiles - R->tile_shard + R->tile_shards - 1) / R->tile_shards)), tblock(64);
+        const dim3 tgrid((unsigned)((n_tiles - R->tile_shard + R->tile_shards - 1) / R->tile_shards)), tblock(64);
         const char* cs = cnt ? "true" : "false";
-        if (wv == 11) {
-            // straggler consolidation: a queue entry per possible hand-off (at most cons_lanes per tile wave), the
-            // control words and the written-flags cleared per render, cons_blocks consumer workgroups after the tiles
-            const size_t cap = (size_t)tgrid.x * (size_t)std::max(1, R->cons_lanes);
-            if (cap > R->cons_cap) {
-                HIP_TRY(hipStreamSynchronize(st));
-                if (R->d_cons_flag) (void)hipFree(R->d_cons_flag);
-                if (R->d_cons_rec) (void)hipFree(R->d_cons_rec);
-                R->d_cons_flag = nullptr;
-                R->d_cons_rec = nullptr;
-                R->cons_cap = 0;
-                if (!R->d_cons_ctl) HIP_TRY(hipMalloc((void**)&R->d_cons_ctl, 4 * sizeof(uint32_t)));
-                HIP_TRY(hipMalloc((void**)&R->d_cons_flag, cap * sizeof(uint32_t)));
-                HIP_TRY(hipMalloc((void**)&R->d_cons_rec, cap * CONS_REC_F4 * sizeof(float4)));
-                R->cons_cap = cap;
-            }
-            HIP_TRY(hipMemsetAsync(R->d_cons_ctl, 0, 4 * sizeof(uint32_t), st));
-            HIP_TRY(hipMemsetAsync(R->d_cons_flag, 0, cap * sizeof(uint32_t), st));
-            P.cons_lanes = R->cons_lanes;
-            P.cons_tiles = (int)tgrid.x;
-            P.cons_cap = (int)cap;
-            P.cons_threshold = R->cons_threshold;
-            P.cons_ctl = R->d_cons_ctl;
-            P.cons_flag = R->d_cons_flag;
-            P.cons_rec = R->d_cons_rec;
-            if (!R->n_cus) HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
-            P.cons_every = R->cons_every >= 2 ? R->cons_every : 0;
-            P.cons_inter = P.cons_every ? (int)tgrid.x / (P.cons_every - 1) : 0;
-            P.cons_min = R->cons_min;
-            tgrid.x += (unsigned)P.cons_inter + (unsigned)(R->cons_blocks >= 0 ? R->cons_blocks : 2 * R->n_cus);
-        }
         HIP_TRY(hipEventRecord(R->ev_main, st));
-        if (wv == 11) {
-            const int w11 = occ >= 7 ? 7 : occ >= 6 ? 6 : 5;
-            std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 11, %d>", cs, w11);
-            if (w11 == 7) {
-                if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 11, 7>), tgrid, tblock, 0, st, P);
-                else hipLaunchKernelGGL((crt_render_kernel<false, 11, 7>), tgrid, tblock, 0, st, P);
-            } else if (w11 == 6) {
-                if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 11, 6>), tgrid, tblock, 0, st, P);
-                else hipLaunchKernelGGL((crt_render_kernel<false, 11, 6>), tgrid, tblock, 0, st, P);
-            } else {
-                if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 11, 5>), tgrid, tblock, 0, st, P);
-                else hipLaunchKernelGGL((crt_render_kernel<false, 11, 5>), tgrid, tblock, 0, st, P);
-            }
-        } else if (occ >= 7) {
+        if (occ >= 7) {
             std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 8, 7>", cs);
             if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 8, 7>), tgrid, tblock, 0, st, P);
             else hipLaunchKernelGGL((crt_render_kernel<false, 8, 7>), tgrid, tblock, 0, st, P);
@@ -4081,32 +3821,6 @@ int crt_renderer_set_drain_threshold(crt_renderer* R, int lanes) {
 int crt_renderer_set_wave_drain(crt_renderer* R, int sixty_fourths) {
     if (!R || sixty_fourths < 1 || sixty_fourths > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "wave drain 1..64");
     R->wave_drain = sixty_fourths;
-    return CRT_OK;
-}
-
-int crt_renderer_set_consolidation(crt_renderer* R, int lanes, int threshold, int blocks) {
-    if (!R || lanes < 0 || lanes > 63 || threshold < 1 || threshold > 64 || blocks < -1 || blocks > (1 << 20))
-        return set_error(CRT_ERR_INVALID_ARGUMENT, "consolidation: lanes 0..63, threshold 1..64, blocks >= -1");
-    R->cons_lanes = lanes;
-    R->cons_threshold = threshold;
-    R->cons_blocks = blocks;
-    return CRT_OK;
-}
-
-int crt_renderer_set_consolidation_interleave(crt_renderer* R, int every, int min_paths) {
-    if (!R || every < 0 || every == 1 || every > 4096 || min_paths < 1 || min_paths > 64)
-        return set_error(CRT_ERR_INVALID_ARGUMENT, "consolidation interleave: every 0 or 2..4096, min_paths 1..64");
-    R->cons_every = every;
-    R->cons_min = min_paths;
-    return CRT_OK;
-}
-
-int crt_renderer_get_consolidation_stats(crt_renderer* R, uint32_t out[4]) {
-    if (!R || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
-    if (!R->d_cons_ctl) { out[0] = out[1] = out[2] = out[3] = 0; return CRT_OK; }
-    HIP_TRY(hipSetDevice(R->device));
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(out, R->d_cons_ctl, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return CRT_OK;
 }
 

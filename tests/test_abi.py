@@ -41,7 +41,7 @@ def test_host_library_exports_header():
 def test_libraries_load_without_gpu():
     from crt_amd import _lib
     L = _lib.hip()
-    assert L.crt_abi_version() == 4
+    assert L.crt_abi_version() == 3
     n = C.c_int(-1)
     assert L.crt_device_count(C.byref(n)) == 0 and n.value >= 0
     _lib.host()

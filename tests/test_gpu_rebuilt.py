@@ -442,44 +442,6 @@ def test_probe_stride_is_bit_identical(rebuilt, stride):
         assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1]) and out[0][2] == out[1][2]
 
 
-@pytest.mark.parametrize("config", ["w4", "w4sbvh"])
-def test_straggler_consolidation_is_bit_identical(rebuilt, config):
-    """Variant 11 (variant 8 + straggler consolidation, crt_renderer_set_consolidation): a tile wave down to a few live
-    lanes hands their paths to a device queue and ends; consumer workgroups finish them 64 at a time.  Each pixel is still
-    traced by one lane at a time, samples in order, on its own RNG stream, so frames, RNG state, the ray count and the
-    counting kernel's box / triangle / sphere tests and paths equal variant 8's; every queued path is taken, no consumer
-    gave up waiting; with and without interleaved consumers, ragged sizes, occupancy 6 and 7, and the SBVH tree."""
-    dev = rebuilt["cornell_bunny", config]
-    for w, h, spp in ((640, 360, 64), (100, 37, 70), (2560, 1440, 64)):
-        out = []
-        # (variant, hand-off lanes, consumer threshold, one interleaved consumer per `every` workgroups, its minimum batch)
-        for variant, lanes, thr, every, mn in ((8, 8, 44, 9, 32), (11, 8, 44, 9, 32), (11, 32, 16, 3, 1),
-                                               (11, 63, 44, 0, 32)):
-            r = crt_amd.Renderer(w, h)
-            r.set_kernel_variant(variant)
-            r.set_consolidation(lanes, thr, -1)
-            r.set_consolidation_interleave(every, mn)
-            r.set_camera(crt_amd.camera(spp))
-            r.init_rand(41)
-            r.render(dev, spp, 20)
-            r.synchronize()
-            assert r.last_kernel_name().startswith(f"crt_render_kernel<false, {variant},")
-            got = (r.linear().view(np.uint32), r.rng_state(), r.counters()["rays"])
-            if variant == 11:
-                st = r.consolidation_stats()
-                assert st["spin_outs"] == 0 and st["taken"] == st["reserved"] and st["reserved"] > 0, st
-                assert st["tile_waves_done"] == ((w + 7) // 8) * ((h + 7) // 8), st
-            r.init_rand(41)
-            r.render(dev, spp, 20, count_work=True)
-            r.synchronize()
-            c = r.counters()
-            out.append(got + ((c["rays"], c["box_tests"], c["tri_tests"], c["sphere_tests"], c["paths"]),))
-        for o in out[1:]:
-            assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1]) and out[0][2] == o[2]
-            assert out[0][3] == o[3], (out[0][3], o[3])
-        assert out[0][3][0] == out[0][2]
-
-
 def test_wave_drain_is_bit_identical(rebuilt):
     """Variants 8 and 4 with draining waves passing at 16/64 and 48/64 (the default) of their live lanes instead of all
     of them (crt_renderer_set_wave_drain): only when lanes run their shading passes changes, so frames, RNG state and ray

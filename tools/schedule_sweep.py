@@ -5,9 +5,7 @@ that share `reps` times, the settings interleaved round by round, and prints per
 time (best and median), the render with the probe and tile sort, and the rays.  Settings are
 `name:key=value,key=value` with keys crit (critical tiles, -1 = auto), lanes (their threshold), T (regeneration
 threshold), occ (waves per SIMD, 0 = auto), stride (probe stride, 0 = auto), probe (probe spp, -1 = auto), wd (the wave
-drain in 64ths, crt_renderer_set_wave_drain), v (kernel variant, -1 = automatic; 11 = variant 8 with straggler
-consolidation), cl / ct / cb / ce / cm (variant 11's hand-off lanes, consumer threshold, trailing consumer blocks,
-one interleaved consumer per ce workgroups (0 = none), their minimum batch).  Results
+drain in 64ths, crt_renderer_set_wave_drain).  Results
 never depend on them; the ray count is printed so that a setting that changed the work would show.
 
     python tools/schedule_sweep.py --world 8 --set base: crit0:crit=0 crit2k:crit=2048 T40:T=40 occ6:occ=6
@@ -36,7 +34,7 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--set", nargs="+", default=["base:"])
 a = ap.parse_args()
 
-DEFAULT = {"crit": -1, "lanes": 16, "T": 44, "occ": 0, "stride": 0, "probe": -1, "wd": 48, "v": -1, "cl": 8, "ct": 44, "cb": -1, "ce": 9, "cm": 32}
+DEFAULT = {"crit": -1, "lanes": 16, "T": 44, "occ": 0, "stride": 0, "probe": -1, "wd": 48}
 settings = []
 for s in a.set:
     name, _, kv = s.partition(":")
@@ -63,18 +61,12 @@ def run(d: dict) -> dict:
     r.set_regen_threshold(d["T"])
     r.set_occupancy_target(d["occ"])
     r.set_wave_drain(d["wd"])
-    r.set_kernel_variant(d["v"])
-    r.set_consolidation(d["cl"], d["ct"], d["cb"])
-    r.set_consolidation_interleave(d["ce"], d["cm"])
     r.init_rand(41, base)
     r.render(sc, spp, a.bounces)
     r.synchronize()
     t = r.last_timings()
-    out = {"main": t["main_kernel_ms"], "render": t["render_ms"], "probe": t["probe_sort_ms"],
-           "rays": r.counters()["rays"], "kernel": r.last_kernel_name()}
-    if d["v"] == 11:
-        out["cons"] = r.consolidation_stats()
-    return out
+    return {"main": t["main_kernel_ms"], "render": t["render_ms"], "probe": t["probe_sort_ms"],
+            "rays": r.counters()["rays"], "kernel": r.last_kernel_name()}
 
 
 run(settings[0][1])   # warm-up (and the RNG jump for this base)
@@ -89,8 +81,7 @@ for name, d in settings:
     out = {"name": name, **{k: v for k, v in d.items() if v != DEFAULT[k]}, "world": a.world, "rank": a.rank,
            "spp": spp, "main_best_ms": round(min(mains), 3), "main_median_ms": round(statistics.median(mains), 3),
            "render_best_ms": round(min(x["render"] for x in xs), 3), "probe_ms": round(xs[-1]["probe"], 3),
-           "rays": xs[-1]["rays"], "kernel": xs[-1]["kernel"], "main_ms_reps": [round(m, 3) for m in mains],
-           "cons": xs[-1].get("cons")}
+           "rays": xs[-1]["rays"], "kernel": xs[-1]["kernel"], "main_ms_reps": [round(m, 3) for m in mains]}
     if ref_main is None:
         ref_main = out["main_median_ms"]
     out["vs_first"] = round(out["main_median_ms"] / ref_main - 1, 4)
