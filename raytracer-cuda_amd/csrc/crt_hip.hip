@@ -1157,24 +1157,6 @@ struct CamRegs {
     int fast_uv;      // uv_div is verified exact for this frame size (crt_renderer_create): no IEEE division
 };
 
-__device__ __forceinline__ CamRegs cam_regs(const RenderParams& P) {
-    const crt_camera_desc& Cd = P.cam;
-    CamRegs C;
-    C.pos = v3(Cd.origin[0], Cd.origin[1], Cd.origin[2]);
-    C.llc = v3(Cd.lower_left[0], Cd.lower_left[1], Cd.lower_left[2]);
-    C.hor = v3(Cd.horizontal[0], Cd.horizontal[1], Cd.horizontal[2]);
-    C.ver = v3(Cd.vertical[0], Cd.vertical[1], Cd.vertical[2]);
-    C.right = v3(Cd.right[0], Cd.right[1], Cd.right[2]);
-    C.up = v3(Cd.up[0], Cd.up[1], Cd.up[2]);
-    C.lens = Cd.lens_radius;
-    C.fw = (float)P.width;
-    C.fh = (float)P.height;
-    C.rfw = P.rcp_w;
-    C.rfh = P.rcp_h;
-    C.fast_uv = P.fast_uv;
-    return C;
-}
-
 // Phase 1: give the lane a ray to trace — Camera::getRay for a new sample, the bounce-limit exit and
 // Russian roulette (CUDAKernels.h:110-121).  Returns false when the pixel has no samples left.
 __device__ __forceinline__ bool next_ray(PathState& S, const CamRegs& C, int x, int y, int max_bounces) {
@@ -1460,22 +1442,26 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         if (P.accumulate) S.pixel = v3(P.sum[3 * (size_t)pix], P.sum[3 * (size_t)pix + 1], P.sum[3 * (size_t)pix + 2]);
         S.remaining = P.spp;
     }
-    // The camera (next_ray's 23 uniform values) is re-read from the kernel arguments where next_ray needs it, through the
-    // kernel-argument segment pointer (taking &P would copy the parameter block to scratch), behind an empty asm so that
-    // the loads stay at the use instead of being hoisted out of the loop: kept in SGPRs across the loop, the camera
-    // pushed the benchmarked kernel to 17 spilled SGPRs (26 v_readlane read-backs, three per stack push or pop) and made
-    // the compiler reload other kernel arguments inside the loop.
-    auto cam = [&]() -> CamRegs {
-        const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();   // C cast: an address-space cast
-        __asm__ volatile("" : "+s"(ka));
-        return cam_regs(*reinterpret_cast<const RenderParams*>(ka));
-    };
+    const crt_camera_desc& Cd = P.cam;
+    CamRegs C;
+    C.pos = v3(Cd.origin[0], Cd.origin[1], Cd.origin[2]);
+    C.llc = v3(Cd.lower_left[0], Cd.lower_left[1], Cd.lower_left[2]);
+    C.hor = v3(Cd.horizontal[0], Cd.horizontal[1], Cd.horizontal[2]);
+    C.ver = v3(Cd.vertical[0], Cd.vertical[1], Cd.vertical[2]);
+    C.right = v3(Cd.right[0], Cd.right[1], Cd.right[2]);
+    C.up = v3(Cd.up[0], Cd.up[1], Cd.up[2]);
+    C.lens = Cd.lens_radius;
+    C.fw = (float)P.width;
+    C.fh = (float)P.height;
+    C.rfw = P.rcp_w;
+    C.rfh = P.rcp_h;
+    C.fast_uv = P.fast_uv;
     TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t wave_rays = 0;    // variant 8: rays of the wave (uniform); the other variants count per lane
 
     if constexpr (VARIANT == 0) {
         for (;;) {
-            if (!next_ray(S, cam(), x, y, P.max_bounces)) break;
+            if (!next_ray(S, C, x, y, P.max_bounces)) break;
             ++S.rays;
             float t;
             const int hit = trace<COUNT>(P.nodes, P.prims, P.n_nodes, layout_base(S.d, P.n_layouts, P.n_nodes), S.o,
@@ -1513,7 +1499,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 if (COUNT) cnt.passes++;
                 if (parked) {
                     if (has_result) finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, c0);
-                    live = next_ray(S, cam(), px, py, P.max_bounces);
+                    live = next_ray(S, C, px, py, P.max_bounces);
                     has_result = false;
                 }
                 if (have && !live) {     // the pixel's samples are done: store it (CUDAKernels.h:162-165)
@@ -1552,7 +1538,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                             S.need_new = true;
                             have = true;
                             rays0_lds[threadIdx.x] = S.rays;
-                            live = next_ray(S, cam(), px, py, P.max_bounces);
+                            live = next_ray(S, C, px, py, P.max_bounces);
                             if (!live) {         // spp == 0: nothing to trace, store as is
                                 uint32_t* w = P.rng + 6 * (size_t)ppix;
                                 w[0] = S.s.v0; w[1] = S.s.v1; w[2] = S.s.v2; w[3] = S.s.v3; w[4] = S.s.v4; w[5] = S.s.d;
@@ -1650,7 +1636,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, s0);
                     }
                     const uint64_t s1 = COUNT ? shader_clock() : 0;
-                    const bool live = next_ray(S, cam(), x, y, P.max_bounces);
+                    const bool live = next_ray(S, C, x, y, P.max_bounces);
                     if (COUNT) {
                         const uint64_t s2 = shader_clock();
                         cnt.cyc_shade += s1 - s0;
@@ -1705,7 +1691,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             if (n_parked >= P.regen_threshold || n_parked == n_live) {
                 if (parked) {
                     if (has_result) shade(S, P, hit, closest);
-                    live = next_ray(S, cam(), x, y, P.max_bounces);
+                    live = next_ray(S, C, x, y, P.max_bounces);
                     has_result = false;
                     if (live) {
                         ++S.rays;
@@ -1730,7 +1716,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     } else {
         bool live = true;
         for (;;) {
-            if (live) live = next_ray(S, cam(), x, y, P.max_bounces);
+            if (live) live = next_ray(S, C, x, y, P.max_bounces);
             if (!wave_ballot(live)) break;
             float t;
             const int hit = trace_coop<COUNT>(P.nodes, P.prims, P.n_nodes, layout_base(S.d, P.n_layouts, P.n_nodes),

@@ -112,7 +112,7 @@ PURPOSES = [
     ("pass: new-ray set-up (1/d, rows, LDS ray)", rng("crt_render_kernel", "if (!TILED) ++S.rays;",
                                                       "L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);")),
     ("pass: live mask + ray count", rng("crt_render_kernel", "live_mask = wave_ballot(has_result);",
-                                        "if (TILED && lane == 0) atomicAdd(&L.rays, (uint32_t)__popcll(parked_mask & live_mask));")),
+                                        "if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);")),
 ]
 FUNC_PURPOSE = {   # whole helper functions
     "wide_boxes": "box arithmetic (wide_boxes)", "box_inv": "pass: new-ray set-up (1/d, rows, LDS ray)",
@@ -143,7 +143,7 @@ HELPERS = {"wide_boxes", "cas", "ovf_slot", "lane_fresh", "node_base", "node_row
            "sphere_root", "sphere_beyond", "sphere_inv", "ref_scene_box", "cannot_refract_exact", "imax", "better",
            "shader_clock"}
 KERNEL_PASS = rng("crt_render_kernel", "const uint64_t parked_mask = live_mask & wave_ballot",
-                  "if (TILED && lane == 0) atomicAdd(&L.rays, (uint32_t)__popcll(parked_mask & live_mask));")
+                  "if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);")
 KERNEL_WIDE = rng("crt_render_kernel", "} else if constexpr (WIDE) {", "} else if constexpr (VARIANT == 2 || VARIANT == 3")
 
 
