@@ -31,14 +31,20 @@ OUT = REPO / "profiles" / "roofline_counters.json"
 
 
 def read_pass(path):
-    vals, dur, name = {}, None, None
+    """Counters of the pass's first render dispatch: the timed frame (bench.py --steps 1 --warmup 0).  bench.py renders
+    one more frame after it, the end-to-end leg (a fresh renderer), which must not be added in."""
+    per, name = {}, None
     for r in csv.DictReader(open(path)):
         if "crt_render_kernel<false," not in r["Kernel_Name"]:
             continue
         name = re.search(r"crt_render_kernel<[^>]*>", r["Kernel_Name"]).group(0)
-        vals[r["Counter_Name"]] = vals.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-        dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    return vals, dur, name
+        d = per.setdefault(int(r["Dispatch_Id"]), {"vals": {}, "dur": None})
+        d["vals"][r["Counter_Name"]] = d["vals"].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        d["dur"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    if not per:
+        return {}, None, None
+    first = per[min(per)]
+    return first["vals"], first["dur"], name
 
 
 def calibration(path):
@@ -63,6 +69,7 @@ def main():
     ap.add_argument("committed_dir")
     ap.add_argument("--calib", default=None)
     ap.add_argument("--key", default=None, help="workload key (default: from the pass log's bench config)")
+    ap.add_argument("--out", default=str(OUT), help="the summary table to update")
     a = ap.parse_args()
     vals, durs, kname = {}, [], None
     rays = None
@@ -105,9 +112,10 @@ def main():
     e["derived"] = {k: round(v, 6) if isinstance(v, float) and v < 1e6 else v for k, v in derived.items()}
     if a.calib:
         e["vl1_calibration"] = calibration(a.calib)
-    table = json.loads(OUT.read_text()) if OUT.exists() else {}
+    out = Path(a.out)
+    table = json.loads(out.read_text()) if out.exists() else {}
     table[key] = e
-    OUT.write_text(json.dumps(table, indent=1, sort_keys=True) + "\n")
+    out.write_text(json.dumps(table, indent=1, sort_keys=True) + "\n")
     print(json.dumps({key: e["derived"]}, indent=1))
 
 
