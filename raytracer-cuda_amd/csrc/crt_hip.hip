@@ -11,7 +11,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -2303,6 +2305,18 @@ inline bool zero_thickness(const float bmin[3], const float bmax[3]) {
     return bmin[0] == bmax[0] || bmin[1] == bmax[1] || bmin[2] == bmax[2];
 }
 
+// CRT_SETUP_TRACE=1: the host stages of scene creation timed on stderr (tools/setup_breakdown.py).
+struct SetupTrace {
+    bool on = std::getenv("CRT_SETUP_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(const char* stage) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[crt setup] %-28s %8.2f ms\n", stage, std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+
 // Flattens the reference's scene + mesh BVHs into the threaded layout and records, per primitive,
 // its reference DFS rank (the order BVHNode::hit / Mesh::hit visit primitives) and whether any box
 // on its path is zero-thickness (then the reference never reports it).
@@ -2460,6 +2474,7 @@ struct Rebuilt {
     // SBVH on the host (crt_sah::SpatialBuilder), width 4 only
     bool build(const Flattener& F, int leaf_size, int layouts, float trav_cost, int wide, int gpu_device = -1,
                bool spatial = false, float alpha = 1e-5f, float max_dup = 1.f) {
+        SetupTrace tr;
         width = wide;
         const int n = (int)(F.prims.size() / 3);
         std::vector<crt_sah::Item> items;
@@ -2560,6 +2575,7 @@ struct Rebuilt {
             }
             return true;
         }
+        tr.lap("  SAH items");
         std::vector<crt_sah::Node> bnv;
         std::vector<crt_sah::Item> its;
         if (spatial) {
@@ -2585,9 +2601,12 @@ struct Rebuilt {
             its = B.items();
         }
         references = (long)its.size();
+        tr.lap(gpu_device >= 0 ? "  SAH build (GPU)" : "  SAH build (host)");
         if (width == 4) {
             if (!emit4(F, bnv, its)) return false;
+            tr.lap("  4-wide collapse + emission");
             append_ray_spheres();
+            tr.lap("  per-ray spheres");
             return true;
         }
         prims.resize(3 * its.size());
@@ -2615,7 +2634,9 @@ private:
         prims.clear();
         // a 4-wide node step costs about one triangle test (the cost probe's weights); node costs 0.5
         // and 2 measured the same (profiles/r02ax)
+        SetupTrace tr;
         const crt_sah::Collapse col(bn, 1.0);
+        tr.lap("    collapse DP");
         for (size_t qi = 0; qi < queue.size(); ++qi) {
             const crt_sah::Wide w = col.open(queue[qi]);
             wide.push_back(w);
@@ -2657,6 +2678,7 @@ private:
             nodes.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
         }
         n_nodes = (int)queue.size();
+        tr.lap("    BFS emission");
         // stack bound: visiting a node with 2+ hit internal children pushes ONE entry (its remaining children)
         if (n_nodes >= (1 << 24)) { err = "too many nodes for 24-bit stack entries"; return false; }
         std::vector<int> bound(n_nodes, 0);
@@ -2838,8 +2860,13 @@ static int build_scene_arrays(const crt_scene_desc* D, const crt_scene_options* 
     if (o.layouts != 1 && o.layouts != 6) return set_error(CRT_ERR_INVALID_ARGUMENT, "layouts must be 1 or 6");
     if (D->n_scene_nodes <= 0 || !D->scene_nodes) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene has no BVH nodes");
     if (D->n_materials < 0 || (D->n_materials > 0 && !D->materials)) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad materials");
-    if (!F.build_triangles() || !F.emit_scene(0, 0, false)) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene: " + F.err);
+    SetupTrace tr;
+    if (!F.build_triangles()) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene: " + F.err);
+    tr.lap("triangle records");
+    if (!F.emit_scene(0, 0, false)) return set_error(CRT_ERR_INVALID_ARGUMENT, "scene: " + F.err);
+    tr.lap("flatten reference BVHs");
     F.finalize_ranks();
+    tr.lap("ranks");
     if (o.bvh == CRT_BVH_REBUILT) {
         if (o.width == 4) o.layouts = 1;
         if (o.spatial_alpha == 0.f) o.spatial_alpha = 1e-5f;
@@ -2850,6 +2877,7 @@ static int build_scene_arrays(const crt_scene_desc* D, const crt_scene_options* 
         if (!RB.build(F, o.leaf_size, o.layouts, o.traversal_cost, o.width, o.gpu_build && !o.spatial_splits ? gpu_device : -1,
                       o.spatial_splits != 0, o.spatial_alpha, o.spatial_max_dup))
             return set_error(CRT_ERR_INVALID_ARGUMENT, "scene: " + RB.err);
+        tr.lap("rebuilt tree (all)");
         if ((size_t)RB.n_nodes * o.layouts * (o.width == 4 ? 8 : 2) >= (size_t)1 << 31)
             return set_error(CRT_ERR_INVALID_ARGUMENT, "scene too large");
     }
@@ -2945,6 +2973,7 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
     Flattener F{D};
     Rebuilt RB;
     if (int rc = build_scene_arrays(D, opts, o, F, RB, device)) return rc;
+    SetupTrace tr;
     const bool rebuilt = o.bvh == CRT_BVH_REBUILT;
     std::vector<float4> mats;
     for (int i = 0; i < D->n_materials; ++i) {
@@ -3003,15 +3032,19 @@ int crt_scene_create_ex(const crt_scene_desc* D, int device, const crt_scene_opt
         for (size_t n = 0; n < RB.nodes.size() / 8; ++n)
             for (size_t k = 0; k < 8; ++k) swizzled[8 * n + (k ^ (n & 7))] = RB.nodes[8 * n + k];
     }
+    tr.lap("node swizzle");
+    const std::vector<float4> shade = shading_records(rc, rebuilt ? RB.prims : F.prims, D);
+    tr.lap("shading records");
     hipError_t e;
     if ((e = up(&S->d_nodes, S->width == 4 ? swizzled : (rebuilt ? RB.nodes : F.nodes))) != hipSuccess ||
         (e = up(&S->d_prims, rebuilt ? RB.prims : F.prims)) != hipSuccess ||
         (e = up(&S->d_mats, mats)) != hipSuccess ||
         (e = up(&S->d_chain, rebuilt ? RB.chain : std::vector<float4>())) != hipSuccess ||
-        (e = up(&S->d_shade, shading_records(rc, rebuilt ? RB.prims : F.prims, D))) != hipSuccess) {
+        (e = up(&S->d_shade, shade)) != hipSuccess) {
         crt_scene_destroy(S);
         return set_error(CRT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e));
     }
+    tr.lap("uploads");
     *out = S;
     return CRT_OK;
 }
