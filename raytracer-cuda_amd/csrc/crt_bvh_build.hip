@@ -763,36 +763,86 @@ __global__ void k_sah_reset(uint32_t* __restrict__ red, int n_lev) {
     red[i] = v;
 }
 
+// Positions per workgroup of k_sah_bounds / k_sah_bins.  A node's items occupy one contiguous range of positions, so a
+// workgroup whose first and last positions belong to the same node holds that node only (the top levels: few nodes of
+// many items).  Such a workgroup reduces in registers and LDS and adds its result to the node's with one global atomic
+// per word; before round 5 every wave (bounds) or every item (bins) did, and the top levels' bins took 1M items x 21
+// atomics on one node's 2,688 words (config E's SAH build: 65 ms of its 100 ms of kernels, profiles/r05l).  Min, max and
+// add are order-independent, so the tree is the same.
+constexpr int SAH_CHUNK = 4096;
+
 // node bounds: item boxes, centroid bounds, sphere count
-__global__ void k_sah_bounds(const int* __restrict__ seg, const uint32_t* __restrict__ perm, const float* __restrict__ ilo,
-                             const float* __restrict__ ihi, const float* __restrict__ ic, const int* __restrict__ isph,
-                             int n, uint32_t* __restrict__ red) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    const LaneSeg L = lane_seg(seg, p, n);
-    if (L.s0 < 0) return;
-    const bool act = L.s >= 0;
-    const uint32_t t = act ? perm[p] : 0;
-    uint32_t v[12];
-    for (int a = 0; a < 3; ++a) {
-        v[a] = act ? ord(ilo[(size_t)a * n + t]) : 0xffffffffu;
-        v[3 + a] = act ? ord(ihi[(size_t)a * n + t]) : 0u;
-        v[6 + a] = act ? ord(ic[(size_t)a * n + t]) : 0xffffffffu;
-        v[9 + a] = act ? ord(ic[(size_t)a * n + t]) : 0u;
-    }
-    const uint32_t sp = act ? (uint32_t)isph[t] : 0u;
-    if (L.uniform) {
-        uint32_t r[12];
-        for (int k = 0; k < 12; ++k) r[k] = ((k % 6) < 3) ? wave_min(v[k]) : wave_max(v[k]);
-        const uint64_t nsp = __ballot(sp != 0);
-        if ((threadIdx.x & 63) == 0) {
-            uint32_t* o = red + (size_t)L.s0 * SAH_RED;
-            for (int k = 0; k < 12; ++k) ((k % 6) < 3) ? atomicMin(&o[k], r[k]) : atomicMax(&o[k], r[k]);
-            if (nsp) atomicAdd(&o[12], (uint32_t)__popcll(nsp));
+__global__ __launch_bounds__(256) void k_sah_bounds(const int* __restrict__ seg, const uint32_t* __restrict__ perm,
+                                                    const float* __restrict__ ilo, const float* __restrict__ ihi,
+                                                    const float* __restrict__ ic, const int* __restrict__ isph, int n,
+                                                    uint32_t* __restrict__ red) {
+    __shared__ uint32_t part[4][13];
+    const int p0 = blockIdx.x * SAH_CHUNK, p1 = min(n, p0 + SAH_CHUNK);
+    const int s_first = seg[p0];
+    if (s_first >= 0 && seg[p1 - 1] == s_first) {   // uniform workgroup: one node
+        uint32_t v[12];
+        for (int k = 0; k < 12; ++k) v[k] = ((k % 6) < 3) ? 0xffffffffu : 0u;
+        uint32_t nsp = 0;
+        for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {
+            const uint32_t t = perm[p];
+            for (int a = 0; a < 3; ++a) {
+                v[a] = min(v[a], ord(ilo[(size_t)a * n + t]));
+                v[3 + a] = max(v[3 + a], ord(ihi[(size_t)a * n + t]));
+                const uint32_t c = ord(ic[(size_t)a * n + t]);
+                v[6 + a] = min(v[6 + a], c);
+                v[9 + a] = max(v[9 + a], c);
+            }
+            nsp += isph[t] != 0;
         }
-    } else if (act) {
-        uint32_t* o = red + (size_t)L.s * SAH_RED;
-        for (int k = 0; k < 12; ++k) ((k % 6) < 3) ? atomicMin(&o[k], v[k]) : atomicMax(&o[k], v[k]);
-        if (sp) atomicAdd(&o[12], 1u);
+        const int w = threadIdx.x >> 6;
+        for (int k = 0; k < 12; ++k) {
+            const uint32_t r = ((k % 6) < 3) ? wave_min(v[k]) : wave_max(v[k]);
+            if ((threadIdx.x & 63) == 0) part[w][k] = r;
+        }
+        uint32_t ns = nsp;
+        for (int o = 32; o > 0; o >>= 1) ns += (uint32_t)__shfl_xor((int)ns, o, 64);
+        if ((threadIdx.x & 63) == 0) part[w][12] = ns;
+        __syncthreads();
+        if (threadIdx.x < 13) {
+            const int k = threadIdx.x;
+            uint32_t r = part[0][k];
+            for (int q = 1; q < 4; ++q)
+                r = k == 12 ? r + part[q][k] : ((k % 6) < 3) ? min(r, part[q][k]) : max(r, part[q][k]);
+            uint32_t* o = red + (size_t)s_first * SAH_RED;
+            if (k == 12) { if (r) atomicAdd(&o[12], r); }
+            else if ((k % 6) < 3) atomicMin(&o[k], r);
+            else atomicMax(&o[k], r);
+        }
+        return;
+    }
+    for (int q = p0; q < p1; q += 256) {   // several nodes: per wave (one node) or per item
+        const int p = q + (int)threadIdx.x;
+        const LaneSeg L = lane_seg(seg, p, p1);
+        if (L.s0 < 0) continue;
+        const bool act = L.s >= 0;
+        const uint32_t t = act ? perm[p] : 0;
+        uint32_t v[12];
+        for (int a = 0; a < 3; ++a) {
+            v[a] = act ? ord(ilo[(size_t)a * n + t]) : 0xffffffffu;
+            v[3 + a] = act ? ord(ihi[(size_t)a * n + t]) : 0u;
+            v[6 + a] = act ? ord(ic[(size_t)a * n + t]) : 0xffffffffu;
+            v[9 + a] = act ? ord(ic[(size_t)a * n + t]) : 0u;
+        }
+        const uint32_t sp = act ? (uint32_t)isph[t] : 0u;
+        if (L.uniform) {
+            uint32_t r[12];
+            for (int k = 0; k < 12; ++k) r[k] = ((k % 6) < 3) ? wave_min(v[k]) : wave_max(v[k]);
+            const uint64_t nsp = __ballot(sp != 0);
+            if ((threadIdx.x & 63) == 0) {
+                uint32_t* o = red + (size_t)L.s0 * SAH_RED;
+                for (int k = 0; k < 12; ++k) ((k % 6) < 3) ? atomicMin(&o[k], r[k]) : atomicMax(&o[k], r[k]);
+                if (nsp) atomicAdd(&o[12], (uint32_t)__popcll(nsp));
+            }
+        } else if (act) {
+            uint32_t* o = red + (size_t)L.s * SAH_RED;
+            for (int k = 0; k < 12; ++k) ((k % 6) < 3) ? atomicMin(&o[k], v[k]) : atomicMax(&o[k], v[k]);
+            if (sp) atomicAdd(&o[12], 1u);
+        }
     }
 }
 
@@ -819,24 +869,59 @@ __device__ __forceinline__ int sah_bin(float c, float clo, float scale) {
     return min(SAH_BINS - 1, (int)((c - clo) * scale));
 }
 
-__global__ void k_sah_bins(const int* __restrict__ seg, const uint32_t* __restrict__ perm, const float* __restrict__ ilo,
-                           const float* __restrict__ ihi, const float* __restrict__ ic, int n, SahLevel N, int base,
-                           uint32_t* __restrict__ red) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    const int s = seg[p];
-    if (s < 0) return;
-    const int X = base + s;
-    const uint32_t t = perm[p];
-    uint32_t lo[3], hi[3];
-    for (int k = 0; k < 3; ++k) { lo[k] = ord(ilo[(size_t)k * n + t]); hi[k] = ord(ihi[(size_t)k * n + t]); }
-    for (int a = 0; a < 3; ++a) {
-        const float sc = N.scale[3 * (size_t)X + a];
-        if (sc == 0.f) continue;
-        const int b = sah_bin(ic[(size_t)a * n + t], N.clo[3 * (size_t)X + a], sc);
-        uint32_t* o = red + (size_t)s * SAH_RED + 13 + (a * SAH_BINS + b) * 7;
-        atomicAdd(&o[0], 1u);
-        for (int k = 0; k < 3; ++k) { atomicMin(&o[1 + k], lo[k]); atomicMax(&o[4 + k], hi[k]); }
+__global__ __launch_bounds__(256) void k_sah_bins(const int* __restrict__ seg, const uint32_t* __restrict__ perm,
+                                                  const float* __restrict__ ilo, const float* __restrict__ ihi,
+                                                  const float* __restrict__ ic, int n, SahLevel N, int base,
+                                                  uint32_t* __restrict__ red) {
+    constexpr int W = 3 * SAH_BINS * 7;
+    __shared__ uint32_t lb[W];   // the workgroup's bins (uniform workgroups): count, lo[3], hi[3] per axis and bin
+    const int p0 = blockIdx.x * SAH_CHUNK, p1 = min(n, p0 + SAH_CHUNK);
+    const int s_first = seg[p0];
+    if (s_first >= 0 && seg[p1 - 1] == s_first) {   // uniform workgroup: one node
+        const int X = base + s_first;
+        float sc[3], clo[3];
+        for (int a = 0; a < 3; ++a) { sc[a] = N.scale[3 * (size_t)X + a]; clo[a] = N.clo[3 * (size_t)X + a]; }
+        for (int i = threadIdx.x; i < W; i += 256) {
+            const int k = i % 7;
+            lb[i] = k == 0 ? 0u : k < 4 ? 0xffffffffu : 0u;
+        }
+        __syncthreads();
+        for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {
+            const uint32_t t = perm[p];
+            uint32_t lo[3], hi[3];
+            for (int k = 0; k < 3; ++k) { lo[k] = ord(ilo[(size_t)k * n + t]); hi[k] = ord(ihi[(size_t)k * n + t]); }
+            for (int a = 0; a < 3; ++a) {
+                if (sc[a] == 0.f) continue;
+                uint32_t* o = lb + (a * SAH_BINS + sah_bin(ic[(size_t)a * n + t], clo[a], sc[a])) * 7;
+                atomicAdd(&o[0], 1u);
+                for (int k = 0; k < 3; ++k) { atomicMin(&o[1 + k], lo[k]); atomicMax(&o[4 + k], hi[k]); }
+            }
+        }
+        __syncthreads();
+        uint32_t* out = red + (size_t)s_first * SAH_RED + 13;
+        for (int b = threadIdx.x; b < 3 * SAH_BINS; b += 256) {
+            const uint32_t* o = lb + b * 7;
+            if (o[0] == 0u) continue;   // an empty bin leaves the node's bin as it is (count 0, empty box)
+            atomicAdd(&out[b * 7], o[0]);
+            for (int k = 0; k < 3; ++k) { atomicMin(&out[b * 7 + 1 + k], o[1 + k]); atomicMax(&out[b * 7 + 4 + k], o[4 + k]); }
+        }
+        return;
+    }
+    for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {   // several nodes: per item
+        const int s = seg[p];
+        if (s < 0) continue;
+        const int X = base + s;
+        const uint32_t t = perm[p];
+        uint32_t lo[3], hi[3];
+        for (int k = 0; k < 3; ++k) { lo[k] = ord(ilo[(size_t)k * n + t]); hi[k] = ord(ihi[(size_t)k * n + t]); }
+        for (int a = 0; a < 3; ++a) {
+            const float sc = N.scale[3 * (size_t)X + a];
+            if (sc == 0.f) continue;
+            const int b = sah_bin(ic[(size_t)a * n + t], N.clo[3 * (size_t)X + a], sc);
+            uint32_t* o = red + (size_t)s * SAH_RED + 13 + (a * SAH_BINS + b) * 7;
+            atomicAdd(&o[0], 1u);
+            for (int k = 0; k < 3; ++k) { atomicMin(&o[1 + k], lo[k]); atomicMax(&o[4 + k], hi[k]); }
+        }
     }
 }
 
@@ -1030,9 +1115,10 @@ int crtx_build_sah_gpu(int device, const std::vector<crt_sah::Item>& items, int 
             BTRY(A.alloc(&d_red, red_cap));
         }
         hipLaunchKernelGGL(k_sah_reset, dim3(blocks((size_t)n_lev * SAH_RED)), dim3(256), 0, st, d_red, n_lev);
-        hipLaunchKernelGGL(k_sah_bounds, dim3(blocks(n)), dim3(256), 0, st, d_seg, d_perm, d_lo, d_hi, d_c, d_sph, n, d_red);
+        const int chunks = (n + SAH_CHUNK - 1) / SAH_CHUNK;
+        hipLaunchKernelGGL(k_sah_bounds, dim3(chunks), dim3(256), 0, st, d_seg, d_perm, d_lo, d_hi, d_c, d_sph, n, d_red);
         hipLaunchKernelGGL(k_sah_prep, dim3(blocks(n_lev)), dim3(256), 0, st, N, base, n_lev, d_red);
-        hipLaunchKernelGGL(k_sah_bins, dim3(blocks(n)), dim3(256), 0, st, d_seg, d_perm, d_lo, d_hi, d_c, n, N, base, d_red);
+        hipLaunchKernelGGL(k_sah_bins, dim3(chunks), dim3(256), 0, st, d_seg, d_perm, d_lo, d_hi, d_c, n, N, base, d_red);
         hipLaunchKernelGGL(k_sah_decide, dim3(blocks(n_lev)), dim3(256), 0, st, N, base, n_lev, d_red, leaf_size, trav_cost);
         hipLaunchKernelGGL(k_sah_scan, dim3(1), dim3(1024), 0, st, N, n_lev, d_irank, d_stats);
         int n_int = 0;

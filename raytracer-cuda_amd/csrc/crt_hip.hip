@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -18,6 +19,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -2317,6 +2319,21 @@ struct SetupTrace {
     }
 };
 
+// The host loops of scene creation that gather or fill one record per primitive run on up to 16 threads (the GPU box's
+// CPU quota; on config E's million triangles they took ~120 ms of its 0.34-s scene creation on one, profiles/r05k).
+// f(b, e) handles the contiguous range [b, e) of [0, n); every index is written by exactly one worker.
+template <class F>
+void parallel_ranges(size_t n, F&& f, size_t min_per_thread = (size_t)1 << 15) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t T = std::min<size_t>(std::min<size_t>(16, hw ? hw : 1), (n + min_per_thread - 1) / min_per_thread);
+    if (T <= 1) { f((size_t)0, n); return; }
+    std::vector<std::thread> th;
+    th.reserve(T - 1);
+    for (size_t t = 1; t < T; ++t) th.emplace_back([&f, n, T, t]() { f(n * t / T, n * (t + 1) / T); });
+    f((size_t)0, n / T);
+    for (auto& x : th) x.join();
+}
+
 // Flattens the reference's scene + mesh BVHs into the threaded layout and records, per primitive,
 // its reference DFS rank (the order BVHNode::hit / Mesh::hit visit primitives) and whether any box
 // on its path is zero-thickness (then the reference never reports it).
@@ -2419,6 +2436,7 @@ struct Flattener {
     }
     bool build_triangles() {
         mesh_prim_base.assign(D->n_meshes, 0);
+        size_t total = 0;
         for (int m = 0; m < D->n_meshes; ++m) {
             const crt_mesh_desc& M = D->meshes[m];
             if ((uint64_t)M.index_offset + M.index_count > D->n_indices ||
@@ -2427,24 +2445,36 @@ struct Flattener {
                 err = "mesh ranges exceed the scene arrays";
                 return false;
             }
-            mesh_prim_base[m] = (int)(prims.size() / 3);
-            for (uint32_t t = 0; t < M.index_count / 3; ++t) {
-                uint32_t iv[3];
-                for (int c = 0; c < 3; ++c) {
-                    iv[c] = D->indices[M.index_offset + 3 * t + c];
-                    if (iv[c] >= M.vertex_count) { err = "vertex index out of range"; return false; }
-                }
-                const float* p0 = D->positions + 3 * ((size_t)M.vertex_offset + iv[0]);
-                const float* p1 = D->positions + 3 * ((size_t)M.vertex_offset + iv[1]);
-                const float* p2 = D->positions + 3 * ((size_t)M.vertex_offset + iv[2]);
-                const float e1[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};   // Mesh.cuh:277
-                const float e2[3] = {p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2]};   // Mesh.cuh:278
-                const uint32_t mat = (uint32_t)(D->face_materials[M.face_offset + t] + (int32_t)M.material_id_offset);
-                prims.push_back(make_float4(p0[0], p0[1], p0[2], e1[0]));
-                prims.push_back(make_float4(e1[1], e1[2], e2[0], e2[1]));
-                prims.push_back(make_float4(e2[2], i2f((int)mat), 0.f, 0.f));
-            }
+            mesh_prim_base[m] = (int)total;
+            total += M.index_count / 3;
         }
+        prims.assign(3 * total, make_float4(0.f, 0.f, 0.f, 0.f));
+        bool bad_index = false;
+        for (int m = 0; m < D->n_meshes; ++m) {
+            const crt_mesh_desc& M = D->meshes[m];
+            float4* out = prims.data() + 3 * (size_t)mesh_prim_base[m];
+            std::atomic<bool> bad{false};
+            parallel_ranges(M.index_count / 3, [&](size_t b, size_t e) {
+                for (size_t t = b; t < e; ++t) {
+                    uint32_t iv[3];
+                    for (int c = 0; c < 3; ++c) {
+                        iv[c] = D->indices[M.index_offset + 3 * t + c];
+                        if (iv[c] >= M.vertex_count) { bad.store(true, std::memory_order_relaxed); iv[c] = 0; }   // reported below
+                    }
+                    const float* p0 = D->positions + 3 * ((size_t)M.vertex_offset + iv[0]);
+                    const float* p1 = D->positions + 3 * ((size_t)M.vertex_offset + iv[1]);
+                    const float* p2 = D->positions + 3 * ((size_t)M.vertex_offset + iv[2]);
+                    const float e1[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};   // Mesh.cuh:277
+                    const float e2[3] = {p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2]};   // Mesh.cuh:278
+                    const uint32_t mat = (uint32_t)(D->face_materials[M.face_offset + t] + (int32_t)M.material_id_offset);
+                    out[3 * t] = make_float4(p0[0], p0[1], p0[2], e1[0]);
+                    out[3 * t + 1] = make_float4(e1[1], e1[2], e2[0], e2[1]);
+                    out[3 * t + 2] = make_float4(e2[2], i2f((int)mat), 0.f, 0.f);
+                }
+            });
+            bad_index = bad_index || bad.load();
+        }
+        if (bad_index) { err = "vertex index out of range"; return false; }
         rank_of.assign(prims.size() / 3, -1);
         reachable.assign(prims.size() / 3, 0);
         return true;
@@ -2603,7 +2633,7 @@ struct Rebuilt {
         references = (long)its.size();
         tr.lap(gpu_device >= 0 ? "  SAH build (GPU)" : "  SAH build (host)");
         if (width == 4) {
-            if (!emit4(F, bnv, its)) return false;
+            if (!emit4(F, bnv, its, !spatial)) return false;
             tr.lap("  4-wide collapse + emission");
             append_ray_spheres();
             tr.lap("  per-ray spheres");
@@ -2628,57 +2658,91 @@ struct Rebuilt {
 private:
     // 4-wide nodes in BFS order (internal children of a node consecutive), primitives re-laid out so the
     // leaf children of every node are consecutive in slot order.  See the node format at wide_boxes().
-    bool emit4(const Flattener& F, const std::vector<crt_sah::Node>& bn, const std::vector<crt_sah::Item>& its) {
-        std::vector<int> queue{0};
-        std::vector<crt_sah::Wide> wide;
+    bool emit4(const Flattener& F, const std::vector<crt_sah::Node>& bn, const std::vector<crt_sah::Item>& its,
+               bool unique_items) {
         prims.clear();
+        SetupTrace tr;
         // a 4-wide node step costs about one triangle test (the cost probe's weights); node costs 0.5
         // and 2 measured the same (profiles/r02ax)
-        SetupTrace tr;
         const crt_sah::Collapse col(bn, 1.0);
         tr.lap("    collapse DP");
-        for (size_t qi = 0; qi < queue.size(); ++qi) {
-            const crt_sah::Wide w = col.open(queue[qi]);
-            wide.push_back(w);
-            const int first_child = (int)queue.size();
-            for (int s = 0; s < w.n_internal; ++s) queue.push_back(w.bin[s]);
-            const int leaf_first = (int)(prims.size() / 3);
-            uint32_t counts = 0;
-            int total_leaf = 0;
-            for (int s = w.n_internal; s < w.n_slots; ++s) {
-                const crt_sah::Node& L = bn[w.bin[s]];
-                if (L.count > 255) { err = "leaf too large"; return false; }
-                counts |= (uint32_t)L.count << (8 * s);
-                total_leaf += L.count;
-                for (int i = L.first; i < L.first + L.count; ++i) {
-                    const int src = its[i].src, np = (int)(prims.size() / 3);
-                    for (int q = 0; q < 3; ++q) prims.push_back(F.prims[3 * src + q]);
-                    rank_code[F.rank_of[src]] = its[i].sphere ? (SPHERE_BIT | np) : np;
+        // BFS one level at a time: the level's cuts (Collapse::open, a few dependent reads of the binary tree each) in
+        // parallel, then its child and primitive offsets in order
+        std::vector<int> queue{0}, first_child_of, leaf_first_of;
+        std::vector<crt_sah::Wide> wide;
+        size_t n_items = 0;
+        for (size_t lb = 0; lb < queue.size();) {
+            const size_t le = queue.size();
+            wide.resize(le);
+            parallel_ranges(le - lb, [&](size_t b, size_t e) {
+                for (size_t qi = lb + b; qi < lb + e; ++qi) wide[qi] = col.open(queue[qi]);
+            }, 4096);
+            for (size_t qi = lb; qi < le; ++qi) {
+                const crt_sah::Wide& w = wide[qi];
+                first_child_of.push_back((int)queue.size());
+                for (int s = 0; s < w.n_internal; ++s) queue.push_back(w.bin[s]);
+                leaf_first_of.push_back((int)n_items);
+                int total_leaf = 0;
+                for (int s = w.n_internal; s < w.n_slots; ++s) {
+                    if (bn[w.bin[s]].count > 255) { err = "leaf too large"; return false; }
+                    total_leaf += bn[w.bin[s]].count;
                 }
+                // node_step4 takes the leaf span from counts * 0x01010101 (byte-wise running sums)
+                if (total_leaf > 255) { err = "leaf children of one node hold more than 255 primitives"; return false; }
+                n_items += (size_t)total_leaf;
+                // prim_test addresses a record as __umul24(index, 48): the 4-wide tree holds fewer than 2^24 primitives
+                if (n_items >= ((size_t)1 << 24)) { err = "the 4-wide tree holds at most 2^24 - 1 primitives"; return false; }
             }
-            // prim_test addresses a record as __umul24(index, 48): the 4-wide tree holds fewer than 2^24 primitives
-            if (prims.size() / 3 >= ((size_t)1 << 24)) { err = "the 4-wide tree holds at most 2^24 - 1 primitives"; return false; }
-            // node_step4 takes the leaf span from counts * 0x01010101 (byte-wise running sums)
-            if (total_leaf > 255) { err = "leaf children of one node hold more than 255 primitives"; return false; }
-            // every span node_step4 can form lies inside the primitive array: the fast kernel relies on it (the checked
-            // build re-checks it on the device)
-            if ((size_t)leaf_first + (size_t)total_leaf > prims.size() / 3) { err = "leaf span outside the primitives"; return false; }
-            float row[6][4];
-            for (int s = 0; s < 4; ++s) {
-                for (int a = 0; a < 3; ++a) {
-                    float lo = 1e30f, hi = 1e30f;   // empty slot: zero-thickness, never hit
-                    if (s < w.n_slots) { lo = bn[w.bin[s]].lo[a]; hi = bn[w.bin[s]].hi[a]; }
-                    row[2 * a][s] = lo;
-                    row[2 * a + 1][s] = hi;
-                }
-            }
-            for (int r = 0; r < 6; ++r) nodes.push_back(make_float4(row[r][0], row[r][1], row[r][2], row[r][3]));
-            nodes.push_back(make_float4(i2f(first_child), i2f(w.n_internal | (w.n_slots << 8)), i2f(leaf_first),
-                                        i2f((int)counts)));
-            nodes.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+            lb = le;
         }
+        const size_t n_wide = queue.size();
+        tr.lap("    node cuts (BFS)");
+        // node records and each primitive position's item (item_at), then the primitive records: every node and every
+        // position is written once.  Every span node_step4 can form (leaf_first + the node's leaf counts) lies inside
+        // the primitive array by construction; the fast kernel relies on it (the checked build re-checks it on the
+        // device).
+        nodes.assign(8 * n_wide, make_float4(0.f, 0.f, 0.f, 0.f));
+        std::vector<int> item_at(n_items);
+        parallel_ranges(n_wide, [&](size_t b, size_t e) {
+            for (size_t qi = b; qi < e; ++qi) {
+                const crt_sah::Wide& w = wide[qi];
+                uint32_t counts = 0;
+                int at = leaf_first_of[qi];
+                for (int s = w.n_internal; s < w.n_slots; ++s) {
+                    const crt_sah::Node& L = bn[w.bin[s]];
+                    counts |= (uint32_t)L.count << (8 * s);
+                    for (int i = L.first; i < L.first + L.count; ++i) item_at[at++] = i;
+                }
+                float4* row = nodes.data() + 8 * qi;
+                for (int a = 0; a < 3; ++a) {
+                    float lo[4], hi[4];
+                    for (int s = 0; s < 4; ++s) {
+                        lo[s] = hi[s] = 1e30f;   // empty slot: zero-thickness, never hit
+                        if (s < w.n_slots) { lo[s] = bn[w.bin[s]].lo[a]; hi[s] = bn[w.bin[s]].hi[a]; }
+                    }
+                    row[2 * a] = make_float4(lo[0], lo[1], lo[2], lo[3]);
+                    row[2 * a + 1] = make_float4(hi[0], hi[1], hi[2], hi[3]);
+                }
+                row[6] = make_float4(i2f(first_child_of[qi]), i2f(w.n_internal | (w.n_slots << 8)), i2f(leaf_first_of[qi]),
+                                     i2f((int)counts));
+            }
+        }, 4096);
+        tr.lap("    node records");
+        prims.reserve(3 * (n_items + kMaxRaySpheres));   // append_ray_spheres adds at most kMaxRaySpheres records
+        prims.resize(3 * n_items);
+        // a primitive referenced by several leaves (spatial splits) keeps the rank code of its last position, as the
+        // sequential emission did; unique items (the binned builders) have one position each, so any order will do
+        auto gather = [&](size_t b, size_t e) {
+            for (size_t np = b; np < e; ++np) {
+                const crt_sah::Item& it = its[item_at[np]];
+                for (int q = 0; q < 3; ++q) prims[3 * np + q] = F.prims[3 * (size_t)it.src + q];
+                rank_code[F.rank_of[it.src]] = it.sphere ? (SPHERE_BIT | (int)np) : (int)np;
+            }
+        };
+        if (unique_items) parallel_ranges(n_items, gather);
+        else gather(0, n_items);
         n_nodes = (int)queue.size();
-        tr.lap("    BFS emission");
+        tr.lap("    primitive gather");
         // stack bound: visiting a node with 2+ hit internal children pushes ONE entry (its remaining children)
         if (n_nodes >= (1 << 24)) { err = "too many nodes for 24-bit stack entries"; return false; }
         std::vector<int> bound(n_nodes, 0);
@@ -2919,50 +2983,52 @@ int crt_scene_export(const crt_scene_desc* D, const crt_scene_options* opts, flo
 static std::vector<float4> shading_records(const std::vector<int>& rank_code, const std::vector<float4>& prims,
                                            const crt_scene_desc* D) {
     std::vector<float4> out(3 * rank_code.size(), make_float4(0.f, 0.f, 0.f, 0.f));
-    for (size_t r = 0; r < rank_code.size(); ++r) {
-        const bool sphere = (rank_code[r] & SPHERE_BIT) != 0;
-        const size_t p = (size_t)(rank_code[r] & ~SPHERE_BIT);
-        const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1], f2 = prims[3 * p + 2];
-        const uint32_t mat = (uint32_t)i2i_host(sphere ? f1.y : f2.y);
-        uint32_t code = SHADE_INVALID;
-        float4 pay = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (mat < (uint32_t)D->n_materials) {
-            const crt_material_desc& M = D->materials[mat];
-            switch (M.type) {
-                case CRT_LAMBERTIAN: code = SHADE_LAMBERT; pay = make_float4(M.albedo[0], M.albedo[1], M.albedo[2], 0.f); break;
-                case CRT_METAL:
-                    code = SHADE_METAL;
-                    pay = make_float4(M.albedo[0], M.albedo[1], M.albedo[2], M.roughness < 1.f ? M.roughness : 1.f);
-                    break;
-                case CRT_DIELECTRIC: {
-                    // Material.cuh:113 ri = front ? 1.0f / ior : ior, and Schlick's r0 = ((1 - ri) / (1 + ri))^2
-                    // (:133-134) for both faces, in IEEE f32 as the device would compute them per hit
-                    code = SHADE_DIELECTRIC;
-                    auto r0 = [](float r) { const float x = (1 - r) / (1 + r); return x * x; };
-                    const float inv = 1.0f / M.ior;
-                    pay = make_float4(M.ior, inv, r0(inv), r0(M.ior));
-                    break;
+    parallel_ranges(rank_code.size(), [&](size_t rb, size_t re) {
+        for (size_t r = rb; r < re; ++r) {
+            const bool sphere = (rank_code[r] & SPHERE_BIT) != 0;
+            const size_t p = (size_t)(rank_code[r] & ~SPHERE_BIT);
+            const float4 f0 = prims[3 * p], f1 = prims[3 * p + 1], f2 = prims[3 * p + 2];
+            const uint32_t mat = (uint32_t)i2i_host(sphere ? f1.y : f2.y);
+            uint32_t code = SHADE_INVALID;
+            float4 pay = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (mat < (uint32_t)D->n_materials) {
+                const crt_material_desc& M = D->materials[mat];
+                switch (M.type) {
+                    case CRT_LAMBERTIAN: code = SHADE_LAMBERT; pay = make_float4(M.albedo[0], M.albedo[1], M.albedo[2], 0.f); break;
+                    case CRT_METAL:
+                        code = SHADE_METAL;
+                        pay = make_float4(M.albedo[0], M.albedo[1], M.albedo[2], M.roughness < 1.f ? M.roughness : 1.f);
+                        break;
+                    case CRT_DIELECTRIC: {
+                        // Material.cuh:113 ri = front ? 1.0f / ior : ior, and Schlick's r0 = ((1 - ri) / (1 + ri))^2
+                        // (:133-134) for both faces, in IEEE f32 as the device would compute them per hit
+                        code = SHADE_DIELECTRIC;
+                        auto r0 = [](float r) { const float x = (1 - r) / (1 + r); return x * x; };
+                        const float inv = 1.0f / M.ior;
+                        pay = make_float4(M.ior, inv, r0(inv), r0(M.ior));
+                        break;
+                    }
+                    case CRT_DIFFUSE_LIGHT:
+                        code = SHADE_LIGHT;
+                        pay = make_float4(M.emission[0], M.emission[1], M.emission[2], 0.f);
+                        break;
+                    default: code = SHADE_NOEMIT; break;
                 }
-                case CRT_DIFFUSE_LIGHT:
-                    code = SHADE_LIGHT;
-                    pay = make_float4(M.emission[0], M.emission[1], M.emission[2], 0.f);
-                    break;
-                default: code = SHADE_NOEMIT; break;
             }
+            float4 a;
+            if (sphere) {
+                a = make_float4(f0.x, f0.y, f0.z, i2f((int)(code | SHADE_SPHERE)));
+                out[3 * r + 2] = make_float4(1 / f0.w, 0.f, 0.f, 0.f);
+            } else {
+                const float ux = f0.w, uy = f1.x, uz = f1.y, vx = f1.z, vy = f1.w, vz = f2.x;
+                const float cx = uy * vz - uz * vy, cy = uz * vx - ux * vz, cz = ux * vy - uy * vx;
+                const float s = 1.0f / std::sqrt(cx * cx + cy * cy + cz * cz);
+                a = make_float4(s * cx, s * cy, s * cz, i2f((int)code));
+            }
+            out[3 * r] = a;
+            out[3 * r + 1] = pay;
         }
-        float4 a;
-        if (sphere) {
-            a = make_float4(f0.x, f0.y, f0.z, i2f((int)(code | SHADE_SPHERE)));
-            out[3 * r + 2] = make_float4(1 / f0.w, 0.f, 0.f, 0.f);
-        } else {
-            const float ux = f0.w, uy = f1.x, uz = f1.y, vx = f1.z, vy = f1.w, vz = f2.x;
-            const float cx = uy * vz - uz * vy, cy = uz * vx - ux * vz, cz = ux * vy - uy * vx;
-            const float s = 1.0f / std::sqrt(cx * cx + cy * cy + cz * cz);
-            a = make_float4(s * cx, s * cy, s * cz, i2f((int)code));
-        }
-        out[3 * r] = a;
-        out[3 * r + 1] = pay;
-    }
+    });
     return out;
 }
 
