@@ -2448,6 +2448,7 @@ struct Flattener {
             mesh_prim_base[m] = (int)total;
             total += M.index_count / 3;
         }
+        prims.reserve(3 * (total + (size_t)std::max(D->n_spheres, 0)));   // emit_scene appends the spheres
         prims.assign(3 * total, make_float4(0.f, 0.f, 0.f, 0.f));
         bool bad_index = false;
         for (int m = 0; m < D->n_meshes; ++m) {
