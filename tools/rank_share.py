@@ -32,6 +32,9 @@ ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--all-ranks", type=int, default=8, help="also time every rank of this world size once")
 ap.add_argument("--probe-stride", type=int, default=0, help="variant 8's probe stride (crt_renderer_set_schedule; 0 = auto)")
+ap.add_argument("--pixel-groups", type=int, default=1,
+                help="P > 1: rank g renders pixel group g %% P (every P-th tile of the cost order, crt_renderer_set_pixel_shard) "
+                     "with the spp share g // P of world/P spp groups")
 a = ap.parse_args()
 
 W, H = a.width, a.height
@@ -45,8 +48,11 @@ scale = crt_amd.pixel_sample_scale(a.spp)
 
 
 def share(world: int, g: int) -> dict:
-    spp = shard_spp(a.spp, world, g)
-    base = subsequence_base(g, W, H)
+    P = a.pixel_groups if world % a.pixel_groups == 0 and world > 1 else 1
+    gs, Q = g // P, world // P
+    spp = shard_spp(a.spp, Q, gs)
+    base = subsequence_base(gs, W, H)
+    r.set_pixel_shard(g % P, P)
     r.init_rand(41, base)        # first init of this (seed, base) runs the jump kernel; the timed ones copy the cache
     r.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -59,7 +65,8 @@ def share(world: int, g: int) -> dict:
     torch.cuda.synchronize()
     wall = time.perf_counter() - t
     ph = r.last_timings()
-    return {"world": world, "rank": g, "spp": spp, "end_to_end_ms": round(e0.elapsed_time(e1), 3),
+    r.set_pixel_shard(0, 1)
+    return {"world": world, "rank": g, "pixel_groups": P, "spp": spp, "end_to_end_ms": round(e0.elapsed_time(e1), 3),
             "wall_ms": round(wall * 1e3, 3), "render_ms": round(ph["render_ms"], 3),
             "probe_sort_ms": round(ph["probe_sort_ms"], 3), "main_kernel_ms": round(ph["main_kernel_ms"], 3),
             "kernel": r.last_kernel_name(), "rays": r.counters()["rays"]}
