@@ -26,6 +26,7 @@
 #include "crt_hip.h"
 #include "crt_device.h"
 #include "crt_sah.h"
+#include "crt/ParallelFor.h"
 
 using namespace crt;
 
@@ -2319,20 +2320,10 @@ struct SetupTrace {
     }
 };
 
-// The host loops of scene creation that gather or fill one record per primitive run on up to 16 threads (the GPU box's
-// CPU quota; on config E's million triangles they took ~120 ms of its 0.34-s scene creation on one, profiles/r05k).
-// f(b, e) handles the contiguous range [b, e) of [0, n); every index is written by exactly one worker.
-template <class F>
-void parallel_ranges(size_t n, F&& f, size_t min_per_thread = (size_t)1 << 15) {
-    const unsigned hw = std::thread::hardware_concurrency();
-    const size_t T = std::min<size_t>(std::min<size_t>(16, hw ? hw : 1), (n + min_per_thread - 1) / min_per_thread);
-    if (T <= 1) { f((size_t)0, n); return; }
-    std::vector<std::thread> th;
-    th.reserve(T - 1);
-    for (size_t t = 1; t < T; ++t) th.emplace_back([&f, n, T, t]() { f(n * t / T, n * (t + 1) / T); });
-    f((size_t)0, n / T);
-    for (auto& x : th) x.join();
-}
+// The host loops of scene creation that gather or fill one record per primitive run on up to 16 threads
+// (CRT::parallel_ranges; on config E's million triangles they took ~120 ms of its 0.34-s scene creation on one,
+// profiles/r05k).
+using CRT::parallel_ranges;
 
 // Flattens the reference's scene + mesh BVHs into the threaded layout and records, per primitive,
 // its reference DFS rank (the order BVHNode::hit / Mesh::hit visit primitives) and whether any box

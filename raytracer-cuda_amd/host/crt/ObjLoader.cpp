@@ -1,11 +1,13 @@
 // ObjLoader.cpp — see ObjLoader.h for the semantics restated.
 #include "ObjLoader.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <thread>
 #include <unordered_map>
 
 namespace CRT {
@@ -124,9 +126,7 @@ bool read_lines(const std::string& path, std::string* buf) {
 }
 
 template <class F>
-void for_each_line(const std::string& buf, F&& fn) {
-    const char* p = buf.data();
-    const char* end = p + buf.size();
+void for_each_line(const char* p, const char* end, F&& fn) {
     while (p < end) {
         const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
         const char* le = nl ? nl : end;
@@ -148,7 +148,7 @@ bool load_mtl(const std::string& path, std::vector<ObjMaterial>* mats, std::unor
             mats->push_back(cur);
         }
     };
-    for_each_line(buf, [&](const char* b, const char* e) {
+    for_each_line(buf.data(), buf.data() + buf.size(), [&](const char* b, const char* e) {
         Tok t{b, e};
         const char *kb, *ke;
         if (!t.next(&kb, &ke) || *kb == '#') return;
@@ -176,6 +176,96 @@ bool load_mtl(const std::string& path, std::vector<ObjMaterial>* mats, std::unor
     return true;
 }
 
+// One contiguous run of whole lines of the file, parsed on its own (LoadObj parses a large file in up to 16 of them
+// at once).  Everything that depends on the lines before the run is left symbolic and resolved in file order when the
+// runs are joined: a negative (relative) face index counts from the run's first vertex, and a face's material is
+// "the state after this run's first k usemtl / mtllib lines".
+struct Event {
+    bool mtllib;
+    std::string text;   // usemtl: the material name; mtllib: the rest of the line
+};
+struct Run {
+    std::vector<float> vertices;
+    std::vector<int32_t> tri;        // 3 vertex indices per triangle
+    std::vector<uint8_t> rel;        // per index: 1 = relative to the run's first vertex (a negative OBJ index)
+    std::vector<int32_t> tri_event;  // per triangle: this run's events before its face
+    std::vector<Event> events;
+    bool zero_index = false;
+};
+
+void parse_run(const char* b, const char* e, Run* R) {
+    struct Corner { int32_t v; uint8_t rel; };
+    std::vector<Corner> face;
+    // capacity for typical lines ("v x y z" >= 8 bytes a vertex, "f a b c" a triangle), so that the runs' vectors do
+    // not reallocate while other threads parse (an unmapped old block interrupts every thread of the process)
+    const size_t bytes = (size_t)(e - b);
+    R->vertices.reserve(bytes / 8);
+    R->tri.reserve(bytes / 6);
+    R->rel.reserve(bytes / 6);
+    R->tri_event.reserve(bytes / 18);
+    for_each_line(b, e, [&](const char* lb, const char* le) {
+        if (R->zero_index) return;
+        Tok t{lb, le};
+        const char *kb, *ke;
+        if (!t.next(&kb, &ke) || *kb == '#') return;
+        const size_t kl = (size_t)(ke - kb);
+        if (kl == 1 && kb[0] == 'v') {
+            R->vertices.push_back(parse_real(t));
+            R->vertices.push_back(parse_real(t));
+            R->vertices.push_back(parse_real(t));
+        } else if (kl == 1 && kb[0] == 'f') {
+            const int nv = (int)(R->vertices.size() / 3);
+            face.clear();
+            const char *fb, *fe;
+            while (t.next(&fb, &fe)) {
+                int idx = atoi(fb);
+                if (idx > 0) face.push_back({idx - 1, 0});
+                else if (idx < 0) face.push_back({nv + idx, 1});   // + the vertices before the run, when joined
+                else { R->zero_index = true; return; }
+            }
+            if (face.size() < 3) return;
+            Corner i0 = face[0], i1, i2 = face[1];
+            for (size_t k = 2; k < face.size(); ++k) {   // fan (0, k-1, k)
+                i1 = i2;
+                i2 = face[k];
+                for (const Corner& c : {i0, i1, i2}) {
+                    R->tri.push_back(c.v);
+                    R->rel.push_back(c.rel);
+                }
+                R->tri_event.push_back((int32_t)R->events.size());
+            }
+        } else if (kl == 6 && memcmp(kb, "usemtl", 6) == 0) {
+            t.skip();
+            std::string name(t.p, t.end);
+            while (!name.empty() && is_space(name.back())) name.pop_back();
+            R->events.push_back({false, std::move(name)});
+        } else if (kl == 6 && memcmp(kb, "mtllib", 6) == 0) {
+            R->events.push_back({true, std::string(t.p, t.end)});
+        }
+    });
+}
+
+// Runs of about `run_bytes` each (CRT_OBJ_RUN_BYTES overrides, for tests), at most 16, cut after a newline.
+std::vector<std::pair<const char*, const char*>> split_runs(const std::string& buf) {
+    size_t run_bytes = (size_t)4 << 20;
+    if (const char* env = std::getenv("CRT_OBJ_RUN_BYTES")) run_bytes = std::max<size_t>(1, std::strtoull(env, nullptr, 10));
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t n = std::max<size_t>(1, std::min<size_t>({(buf.size() + run_bytes - 1) / run_bytes, 16, hw ? hw : 1}));
+    std::vector<std::pair<const char*, const char*>> runs;
+    const char* p = buf.data();
+    const char* end = p + buf.size();
+    for (size_t k = 1; k <= n && p < end; ++k) {
+        const char* q = k == n ? end : std::max(p, buf.data() + buf.size() * k / n);
+        if (q < end) {
+            const char* nl = (const char*)memchr(q, '\n', (size_t)(end - q));
+            q = nl ? nl + 1 : end;
+        }
+        runs.push_back({p, q});
+        p = q;
+    }
+    return runs;
+}
+
 }  // namespace
 
 bool LoadObj(ObjData* out, std::string* err, const char* filename, const char* mtl_basedir) {
@@ -185,55 +275,68 @@ bool LoadObj(ObjData* out, std::string* err, const char* filename, const char* m
         if (err) *err = std::string("Cannot open file [") + filename + "]";
         return false;
     }
+    const auto spans = split_runs(buf);
+    std::vector<Run> runs(spans.size());
+    {
+        std::vector<std::thread> th;
+        for (size_t k = 1; k < spans.size(); ++k)
+            th.emplace_back(parse_run, spans[k].first, spans[k].second, &runs[k]);
+        if (!spans.empty()) parse_run(spans[0].first, spans[0].second, &runs[0]);
+        for (auto& x : th) x.join();
+    }
+    // join in file order: the usemtl / mtllib lines in sequence (mtllib loads materials that later usemtl lines look up),
+    // then each run's vertices and triangles
     std::unordered_map<std::string, int> mat_map;
     int cur_mat = -1;
-    bool ok = true;
-    std::vector<int32_t> face;
-    for_each_line(buf, [&](const char* b, const char* e) {
-        if (!ok) return;
-        Tok t{b, e};
-        const char *kb, *ke;
-        if (!t.next(&kb, &ke) || *kb == '#') return;
-        const size_t kl = (size_t)(ke - kb);
-        if (kl == 1 && kb[0] == 'v') {
-            out->vertices.push_back(parse_real(t));
-            out->vertices.push_back(parse_real(t));
-            out->vertices.push_back(parse_real(t));
-        } else if (kl == 1 && kb[0] == 'f') {
-            const int nv = (int)(out->vertices.size() / 3);
-            face.clear();
-            const char *fb, *fe;
-            while (t.next(&fb, &fe)) {
-                int idx = atoi(fb);
-                if (idx > 0) face.push_back(idx - 1);
-                else if (idx < 0) face.push_back(nv + idx);
-                else { ok = false; if (err) *err = "zero face index"; return; }
-            }
-            if (face.size() < 3) return;
-            int i0 = face[0], i1, i2 = face[1];
-            for (size_t k = 2; k < face.size(); ++k) {
-                i1 = i2;
-                i2 = face[k];
-                out->triIndices.push_back(i0);
-                out->triIndices.push_back(i1);
-                out->triIndices.push_back(i2);
-                out->triMaterial.push_back(cur_mat);
-            }
-        } else if (kl == 6 && memcmp(kb, "usemtl", 6) == 0) {
-            t.skip();
-            std::string name(t.p, t.end);
-            while (!name.empty() && is_space(name.back())) name.pop_back();
-            auto it = mat_map.find(name);
-            cur_mat = (it != mat_map.end()) ? it->second : -1;
-        } else if (kl == 6 && memcmp(kb, "mtllib", 6) == 0) {
-            const char *fb, *fe;
-            while (t.next(&fb, &fe)) {
-                std::string path = std::string(mtl_basedir ? mtl_basedir : "") + std::string(fb, fe);
-                if (load_mtl(path, &out->materials, &mat_map)) break;
-            }
+    size_t n_vert = 0, n_tri = 0;
+    std::vector<std::vector<int32_t>> mat_after(runs.size());
+    for (size_t k = 0; k < runs.size(); ++k) {
+        const Run& R = runs[k];
+        if (R.zero_index) {
+            if (err) *err = "zero face index";
+            return false;
         }
-    });
-    return ok;
+        auto& ma = mat_after[k];
+        ma.push_back(cur_mat);
+        for (const Event& ev : R.events) {
+            if (ev.mtllib) {
+                Tok t{ev.text.data(), ev.text.data() + ev.text.size()};
+                const char *fb, *fe;
+                while (t.next(&fb, &fe)) {
+                    std::string path = std::string(mtl_basedir ? mtl_basedir : "") + std::string(fb, fe);
+                    if (load_mtl(path, &out->materials, &mat_map)) break;
+                }
+            } else {
+                auto it = mat_map.find(ev.text);
+                cur_mat = (it != mat_map.end()) ? it->second : -1;
+            }
+            ma.push_back(cur_mat);
+        }
+        n_vert += R.vertices.size();
+        n_tri += R.tri_event.size();
+    }
+    out->vertices.resize(n_vert);
+    out->triIndices.resize(3 * n_tri);
+    out->triMaterial.resize(n_tri);
+    {
+        std::vector<std::thread> th;
+        size_t vb = 0, tb = 0;
+        for (size_t k = 0; k < runs.size(); ++k) {
+            auto fill = [&, k, vb, tb]() {
+                const Run& R = runs[k];
+                std::copy(R.vertices.begin(), R.vertices.end(), out->vertices.begin() + vb);
+                const int32_t vbase = (int32_t)(vb / 3);
+                for (size_t i = 0; i < R.tri.size(); ++i) out->triIndices[3 * tb + i] = R.rel[i] ? vbase + R.tri[i] : R.tri[i];
+                for (size_t i = 0; i < R.tri_event.size(); ++i) out->triMaterial[tb + i] = mat_after[k][R.tri_event[i]];
+            };
+            if (k + 1 < runs.size()) th.emplace_back(fill);
+            else fill();
+            vb += runs[k].vertices.size();
+            tb += runs[k].tri_event.size();
+        }
+        for (auto& x : th) x.join();
+    }
+    return true;
 }
 
 }  // namespace CRT

@@ -2,12 +2,30 @@
 // unless noted.
 #include "SceneManager.h"
 
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <limits>
 #include <set>
 #include <stdexcept>
 
 #include "ObjLoader.h"
+#include "ParallelFor.h"
+
+namespace {
+// CRT_SETUP_TRACE=1: the host loader's stages on stderr (tools/setup_breakdown.py; crt_hip.hip times the rest)
+struct LoadTrace {
+    bool on = std::getenv("CRT_SETUP_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(const char* stage) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[crt load]  %-27s %8.2f ms\n", stage, std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+}  // namespace
 
 SceneManager::SceneManager(int width, int height, int device) : m_Width(width), m_Height(height), m_Device(device) {}
 
@@ -62,29 +80,54 @@ bool SceneManager::buildMeshOnDevice(int i, const float* pos, uint32_t* idx, int
 
 // :100-196
 void SceneManager::initMeshes() {
+    LoadTrace tr;
     std::vector<MeshData> allMeshData;
     for (const auto& file : m_ModelFiles) loadObject(file, allMeshData);
-    m_MeshData = allMeshData;
-    const int n = (int)allMeshData.size();
+    tr.lap("OBJ files (all)");
+    m_MeshData = std::move(allMeshData);
+    const std::vector<MeshData>& meshes = m_MeshData;
+    const int n = (int)meshes.size();
     m_VertexOffsets.assign(n, 0); m_IndexOffsets.assign(n, 0); m_VertexCounts.assign(n, 0);
     m_IndexCounts.assign(n, 0); m_FaceMatOffsets.assign(n, 0); m_FaceCounts.assign(n, 0);
     std::vector<uint32_t> uniquePerMesh;
     m_Positions.clear(); m_Indices.clear(); m_FaceMats.clear();
+    size_t n_vert = 0, n_idx = 0, n_fm = 0;
+    for (const MeshData& md : meshes) { n_vert += md.vertices.size(); n_idx += md.indices.size(); n_fm += md.faceMaterialIds.size(); }
+    m_Positions.resize(3 * n_vert);
+    m_Indices.reserve(n_idx);
+    m_FaceMats.reserve(n_fm);
     for (int i = 0; i < n; i++) {
-        const MeshData& md = allMeshData[i];
-        m_VertexOffsets[i] = (uint32_t)(m_Positions.size() / 3);
+        const MeshData& md = meshes[i];
+        m_VertexOffsets[i] = i == 0 ? 0u : m_VertexOffsets[i - 1] + (uint32_t)meshes[i - 1].vertices.size();
         m_IndexOffsets[i] = (uint32_t)m_Indices.size();
         m_FaceMatOffsets[i] = (uint32_t)m_FaceMats.size();
-        for (const Vertex& v : md.vertices)
-            for (int c = 0; c < 3; ++c) m_Positions.push_back(v.Position[c]);
+        float* pos = m_Positions.data() + 3 * (size_t)m_VertexOffsets[i];
+        CRT::parallel_ranges(md.vertices.size(), [&](size_t b, size_t e) {
+            for (size_t v = b; v < e; ++v)
+                for (int c = 0; c < 3; ++c) pos[3 * v + c] = md.vertices[v].Position[c];
+        });
         m_Indices.insert(m_Indices.end(), md.indices.begin(), md.indices.end());
         m_FaceMats.insert(m_FaceMats.end(), md.faceMaterialIds.begin(), md.faceMaterialIds.end());
-        std::set<int> uniq(md.faceMaterialIds.begin(), md.faceMaterialIds.end());   // :143-145
-        uniquePerMesh.push_back((uint32_t)uniq.size());
+        // :143-145 std::set of the face material ids: its size.  loadObject clamps every id into [0, materials), so
+        // a flag per material counts the same distinct values (other ids, which it never produces, go to a set)
+        std::vector<char> seen;
+        std::set<int> other;
+        uint32_t distinct = 0;
+        for (int id : md.faceMaterialIds) {
+            if (id < 0 || id >= (1 << 20)) {
+                distinct += other.insert(id).second ? 1u : 0u;
+                continue;
+            }
+            if ((size_t)id >= seen.size()) seen.resize((size_t)id + 1, 0);
+            distinct += !seen[(size_t)id];
+            seen[(size_t)id] = 1;
+        }
+        uniquePerMesh.push_back(distinct);
         m_VertexCounts[i] = (uint32_t)md.vertices.size();
         m_IndexCounts[i] = (uint32_t)md.indices.size();
         m_FaceCounts[i] = (uint32_t)md.faceMaterialIds.size();
     }
+    tr.lap("mesh arrays");
     m_MaterialIDOffsets.assign(n, 0);
     m_Meshes.assign(n, crt_mesh_desc{});
     m_MeshBVH.assign(n, {});
@@ -103,6 +146,7 @@ void SceneManager::initMeshes() {
                                                 &m_MeshBVH[i]);
         if (!st.ok) throw std::runtime_error(st.error);
     }
+    tr.lap("mesh BVHs");
     for (int i = 0; i < n; i++) {
         crt_mesh_desc& d = m_Meshes[i];
         d.vertex_offset = m_VertexOffsets[i];
@@ -125,10 +169,12 @@ void SceneManager::loadObject(const std::string& filename, std::vector<MeshData>
     std::string base_dir = last != std::string::npos ? filename.substr(0, last + 1) : "./";
     CRT::ObjData od;
     std::string err;
+    LoadTrace tr;
     if (!CRT::LoadObj(&od, &err, filename.c_str(), base_dir.c_str())) {
         if (!err.empty()) std::cerr << "ObjLoader error:   " << err << std::endl;
         throw std::runtime_error("Failed to load object: " + filename);
     }
+    tr.lap("  LoadObj");
     for (const auto& mat : od.materials) {                                           // :222-247
         CRT::MaterialType mt = CRT::MaterialType::Lambertian;
         if (mat.emission[0] > 0.f || mat.emission[1] > 0.f || mat.emission[2] > 0.f) mt = CRT::MaterialType::DiffuseLight;
@@ -146,33 +192,60 @@ void SceneManager::loadObject(const std::string& filename, std::vector<MeshData>
     MeshData meshData;
     const size_t nTri = od.triMaterial.size();
     if (nTri > 0) meshData.vertices.resize(od.vertices.size());                         // :253 (3x too many slots)
-    for (size_t f = 0; f < nTri; ++f) {
-        int faceMatId = od.triMaterial[f];                                            // :259-265
-        if (faceMatId < 0 || faceMatId >= static_cast<int>(m_SceneMaterialsData.size())) faceMatId = 0;
-        meshData.faceMaterialIds.push_back(faceMatId);
-        for (int v = 0; v < 3; v++) {
-            const int32_t vi = od.triIndices[3 * f + v];
-            if (vi < 0 || 3 * (size_t)vi + 2 >= od.vertices.size())
-                throw std::runtime_error("face vertex index out of range in " + filename);
-            Vertex vertex{};
-            vertex.Position = CRT::Vec3(od.vertices[3 * vi], od.vertices[3 * vi + 1], od.vertices[3 * vi + 2]);
-            meshData.indices.push_back((uint32_t)vi);
-            meshData.vertices[vi] = vertex;                                           // :300 last write wins
-        }
+    for (size_t k = 0; k < 3 * nTri; ++k) {
+        const int32_t vi = od.triIndices[k];
+        if (vi < 0 || 3 * (size_t)vi + 2 >= od.vertices.size())
+            throw std::runtime_error("face vertex index out of range in " + filename);
     }
-    meshDataList.push_back(meshData);
-    // :307-325 — normalise every mesh loaded so far
+    meshData.faceMaterialIds.resize(nTri);
+    meshData.indices.resize(3 * nTri);
+    const int n_mats = static_cast<int>(m_SceneMaterialsData.size());
+    CRT::parallel_ranges(nTri, [&](size_t b, size_t e) {
+        for (size_t f = b; f < e; ++f) {
+            int faceMatId = od.triMaterial[f];                                        // :259-265
+            if (faceMatId < 0 || faceMatId >= n_mats) faceMatId = 0;
+            meshData.faceMaterialIds[f] = faceMatId;
+            for (int v = 0; v < 3; v++) meshData.indices[3 * f + v] = (uint32_t)od.triIndices[3 * f + v];
+        }
+    });
+    // :300 vertices[vi] = the face's vertex, last write wins: every face writes vertex vi's own position, so the slot
+    // of each referenced index gets od.vertices[vi] (the rest stay zero)
+    std::vector<char> used(od.vertices.size() / 3, 0);
+    for (size_t k = 0; k < 3 * nTri; ++k) used[(size_t)od.triIndices[k]] = 1;
+    CRT::parallel_ranges(used.size(), [&](size_t b, size_t e) {
+        for (size_t vi = b; vi < e; ++vi)
+            if (used[vi]) meshData.vertices[vi].Position = CRT::Vec3(od.vertices[3 * vi], od.vertices[3 * vi + 1], od.vertices[3 * vi + 2]);
+    });
+    tr.lap("  mesh data");
+    meshDataList.push_back(std::move(meshData));
+    // :307-325 — normalise every mesh loaded so far.  The bounds fold over the meshes' vertices in order, per range
+    // and then over the ranges in order: fmin / fmax return the same operand on ties either way, so the result is the
+    // sequential fold's
     CRT::Vec3 minBounds(std::numeric_limits<float>::max());
     CRT::Vec3 maxBounds(std::numeric_limits<float>::lowest());
-    for (auto& md : meshDataList)
-        for (const auto& vertex : md.vertices) {
-            minBounds = CRT::Vec3::min(minBounds, vertex.Position);
-            maxBounds = CRT::Vec3::max(maxBounds, vertex.Position);
+    for (auto& md : meshDataList) {
+        std::vector<CRT::Vec3> lo(16, CRT::Vec3(std::numeric_limits<float>::max()));
+        std::vector<CRT::Vec3> hi(16, CRT::Vec3(std::numeric_limits<float>::lowest()));
+        const size_t R = CRT::parallel_ranges_indexed(md.vertices.size(), [&](size_t r, size_t b, size_t e) {
+            CRT::Vec3 l = lo[r], h = hi[r];
+            for (size_t v = b; v < e; ++v) {
+                l = CRT::Vec3::min(l, md.vertices[v].Position);
+                h = CRT::Vec3::max(h, md.vertices[v].Position);
+            }
+            lo[r] = l;
+            hi[r] = h;
+        });
+        for (size_t r = 0; r < R; ++r) {
+            minBounds = CRT::Vec3::min(minBounds, lo[r]);
+            maxBounds = CRT::Vec3::max(maxBounds, hi[r]);
         }
+    }
     CRT::Vec3 center = (minBounds + maxBounds) * 0.5f;
     float scale = 0.6f / (maxBounds - minBounds).maxComponent();
     for (auto& md : meshDataList)
-        for (auto& vertex : md.vertices) vertex.Position = (vertex.Position - center) * scale;
+        CRT::parallel_ranges(md.vertices.size(), [&](size_t b, size_t e) {
+            for (size_t v = b; v < e; ++v) md.vertices[v].Position = (md.vertices[v].Position - center) * scale;
+        });
 }
 
 // createRandomWorld (CUDAKernels.h:28-84) + createBVH (:86-90)
