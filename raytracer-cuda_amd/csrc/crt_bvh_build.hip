@@ -715,6 +715,7 @@ extern "C" int crt_build_mesh_bvh(int device, const float* positions, uint32_t v
 // of items inside a node can differ — any order is a valid tree for the rank rule.
 // ======================================================================================================
 #include "crt_sah.h"
+#include "crt/ParallelFor.h"
 
 namespace {
 
@@ -1057,14 +1058,16 @@ int crtx_build_sah_gpu(int device, const std::vector<crt_sah::Item>& items, int 
     hipStream_t st = nullptr;
     std::vector<float> h(9 * (size_t)n);
     std::vector<int> hs((size_t)n);
-    for (int i = 0; i < n; ++i) {
-        for (int a = 0; a < 3; ++a) {
-            h[(size_t)a * n + i] = items[i].lo[a];
-            h[3 * (size_t)n + (size_t)a * n + i] = items[i].hi[a];
-            h[6 * (size_t)n + (size_t)a * n + i] = items[i].c[a];
+    CRT::parallel_ranges((size_t)n, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) {
+            for (int a = 0; a < 3; ++a) {
+                h[(size_t)a * n + i] = items[i].lo[a];
+                h[3 * (size_t)n + (size_t)a * n + i] = items[i].hi[a];
+                h[6 * (size_t)n + (size_t)a * n + i] = items[i].c[a];
+            }
+            hs[i] = items[i].sphere ? 1 : 0;
         }
-        hs[i] = items[i].sphere ? 1 : 0;
-    }
+    });
     float* d_item = nullptr;
     int* d_sph = nullptr;
     BTRY(A.alloc(&d_item, 9 * (size_t)n));
@@ -1150,14 +1153,16 @@ int crtx_build_sah_gpu(int device, const std::vector<crt_sah::Item>& items, int 
     BTRY(hipMemcpy(hhi.data(), N.hi, (size_t)total * 12, hipMemcpyDeviceToHost));
     BTRY(hipMemcpy(hperm.data(), d_perm, (size_t)n * 4, hipMemcpyDeviceToHost));
     nodes_out->assign((size_t)total, crt_sah::Node{});
-    for (int t = 0; t < total; ++t) {
-        crt_sah::Node& o = (*nodes_out)[t];
-        for (int a = 0; a < 3; ++a) { o.lo[a] = hlo[3 * (size_t)t + a]; o.hi[a] = hhi[3 * (size_t)t + a]; }
-        o.child[0] = hleft[t];
-        o.child[1] = hleft[t] < 0 ? -1 : hleft[t] + 1;
-        o.first = hstart[t];
-        o.count = hleft[t] < 0 ? hcount[t] : 0;
-    }
+    CRT::parallel_ranges((size_t)total, [&](size_t b, size_t e) {
+        for (size_t t = b; t < e; ++t) {
+            crt_sah::Node& o = (*nodes_out)[t];
+            for (int a = 0; a < 3; ++a) { o.lo[a] = hlo[3 * t + a]; o.hi[a] = hhi[3 * t + a]; }
+            o.child[0] = hleft[t];
+            o.child[1] = hleft[t] < 0 ? -1 : hleft[t] + 1;
+            o.first = hstart[t];
+            o.count = hleft[t] < 0 ? hcount[t] : 0;
+        }
+    });
     order_out->assign(hperm.begin(), hperm.end());
     if (max_depth) *max_depth = (int)level_off.size() - 2;
     return CRT_OK;
