@@ -776,11 +776,13 @@ constexpr int SAH_CHUNK = 4096;
 __global__ __launch_bounds__(256) void k_sah_bounds(const int* __restrict__ seg, const uint32_t* __restrict__ perm,
                                                     const float* __restrict__ ilo, const float* __restrict__ ihi,
                                                     const float* __restrict__ ic, const int* __restrict__ isph, int n,
-                                                    uint32_t* __restrict__ red) {
+                                                    const int* __restrict__ big, uint32_t* __restrict__ red) {
     __shared__ uint32_t part[4][13];
     const int p0 = blockIdx.x * SAH_CHUNK, p1 = min(n, p0 + SAH_CHUNK);
     const int s_first = seg[p0];
     if (s_first >= 0 && seg[p1 - 1] == s_first) {   // uniform workgroup: one node
+        const int rb = big[s_first];
+        if (rb < 0) return;                          // a small node: k_sah_small
         uint32_t v[12];
         for (int k = 0; k < 12; ++k) v[k] = ((k % 6) < 3) ? 0xffffffffu : 0u;
         uint32_t nsp = 0;
@@ -809,7 +811,7 @@ __global__ __launch_bounds__(256) void k_sah_bounds(const int* __restrict__ seg,
             uint32_t r = part[0][k];
             for (int q = 1; q < 4; ++q)
                 r = k == 12 ? r + part[q][k] : ((k % 6) < 3) ? min(r, part[q][k]) : max(r, part[q][k]);
-            uint32_t* o = red + (size_t)s_first * SAH_RED;
+            uint32_t* o = red + (size_t)rb * SAH_RED;
             if (k == 12) { if (r) atomicAdd(&o[12], r); }
             else if ((k % 6) < 3) atomicMin(&o[k], r);
             else atomicMax(&o[k], r);
@@ -818,7 +820,14 @@ __global__ __launch_bounds__(256) void k_sah_bounds(const int* __restrict__ seg,
     }
     for (int q = p0; q < p1; q += 256) {   // several nodes: per wave (one node) or per item
         const int p = q + (int)threadIdx.x;
-        const LaneSeg L = lane_seg(seg, p, p1);
+        LaneSeg L;                          // over big-node indices (small nodes' positions: -1)
+        {
+            const int s = p < p1 ? seg[p] : -1;
+            L.s = s >= 0 ? big[s] : -1;
+            const int hi = wave_max_i(L.s), lo = wave_min_i(L.s >= 0 ? L.s : 0x7fffffff);
+            L.uniform = hi >= 0 && lo == hi;
+            L.s0 = hi;
+        }
         if (L.s0 < 0) continue;
         const bool act = L.s >= 0;
         const uint32_t t = act ? perm[p] : 0;
@@ -848,11 +857,11 @@ __global__ __launch_bounds__(256) void k_sah_bounds(const int* __restrict__ seg,
 }
 
 // per node: padded box, bin parameters (crt_sah.h build_range)
-__global__ void k_sah_prep(SahLevel N, int base, int n_lev, const uint32_t* __restrict__ red) {
+__global__ void k_sah_prep(SahLevel N, int base, int n_lev, const int* __restrict__ big, const uint32_t* __restrict__ red) {
     const int li = blockIdx.x * blockDim.x + threadIdx.x;
-    if (li >= n_lev) return;
+    if (li >= n_lev || big[li] < 0) return;
     const int X = base + li;
-    const uint32_t* r = red + (size_t)li * SAH_RED;
+    const uint32_t* r = red + (size_t)big[li] * SAH_RED;
     float lo[3], hi[3];
     for (int a = 0; a < 3; ++a) { lo[a] = unord(r[a]); hi[a] = unord(r[3 + a]); }
     pad_box_dev(lo, hi);
@@ -873,12 +882,14 @@ __device__ __forceinline__ int sah_bin(float c, float clo, float scale) {
 __global__ __launch_bounds__(256) void k_sah_bins(const int* __restrict__ seg, const uint32_t* __restrict__ perm,
                                                   const float* __restrict__ ilo, const float* __restrict__ ihi,
                                                   const float* __restrict__ ic, int n, SahLevel N, int base,
-                                                  uint32_t* __restrict__ red) {
+                                                  const int* __restrict__ big, uint32_t* __restrict__ red) {
     constexpr int W = 3 * SAH_BINS * 7;
     __shared__ uint32_t lb[W];   // the workgroup's bins (uniform workgroups): count, lo[3], hi[3] per axis and bin
     const int p0 = blockIdx.x * SAH_CHUNK, p1 = min(n, p0 + SAH_CHUNK);
     const int s_first = seg[p0];
     if (s_first >= 0 && seg[p1 - 1] == s_first) {   // uniform workgroup: one node
+        const int rb = big[s_first];
+        if (rb < 0) return;                          // a small node: k_sah_small
         const int X = base + s_first;
         float sc[3], clo[3];
         for (int a = 0; a < 3; ++a) { sc[a] = N.scale[3 * (size_t)X + a]; clo[a] = N.clo[3 * (size_t)X + a]; }
@@ -899,7 +910,7 @@ __global__ __launch_bounds__(256) void k_sah_bins(const int* __restrict__ seg, c
             }
         }
         __syncthreads();
-        uint32_t* out = red + (size_t)s_first * SAH_RED + 13;
+        uint32_t* out = red + (size_t)rb * SAH_RED + 13;
         for (int b = threadIdx.x; b < 3 * SAH_BINS; b += 256) {
             const uint32_t* o = lb + b * 7;
             if (o[0] == 0u) continue;   // an empty bin leaves the node's bin as it is (count 0, empty box)
@@ -910,7 +921,7 @@ __global__ __launch_bounds__(256) void k_sah_bins(const int* __restrict__ seg, c
     }
     for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {   // several nodes: per item
         const int s = seg[p];
-        if (s < 0) continue;
+        if (s < 0 || big[s] < 0) continue;
         const int X = base + s;
         const uint32_t t = perm[p];
         uint32_t lo[3], hi[3];
@@ -919,7 +930,7 @@ __global__ __launch_bounds__(256) void k_sah_bins(const int* __restrict__ seg, c
             const float sc = N.scale[3 * (size_t)X + a];
             if (sc == 0.f) continue;
             const int b = sah_bin(ic[(size_t)a * n + t], N.clo[3 * (size_t)X + a], sc);
-            uint32_t* o = red + (size_t)s * SAH_RED + 13 + (a * SAH_BINS + b) * 7;
+            uint32_t* o = red + (size_t)big[s] * SAH_RED + 13 + (a * SAH_BINS + b) * 7;
             atomicAdd(&o[0], 1u);
             for (int k = 0; k < 3; ++k) { atomicMin(&o[1 + k], lo[k]); atomicMax(&o[4 + k], hi[k]); }
         }
@@ -927,12 +938,12 @@ __global__ __launch_bounds__(256) void k_sah_bins(const int* __restrict__ seg, c
 }
 
 // SAH sweep and leaf test (crt_sah.h build_range, same float expressions)
-__global__ void k_sah_decide(SahLevel N, int base, int n_lev, const uint32_t* __restrict__ red, int leaf_size,
-                             float trav_cost) {
+__global__ void k_sah_decide(SahLevel N, int base, int n_lev, const int* __restrict__ big, const uint32_t* __restrict__ red,
+                             int leaf_size, float trav_cost) {
     const int li = blockIdx.x * blockDim.x + threadIdx.x;
-    if (li >= n_lev) return;
+    if (li >= n_lev || big[li] < 0) return;
     const int X = base + li;
-    const uint32_t* r = red + (size_t)li * SAH_RED;
+    const uint32_t* r = red + (size_t)big[li] * SAH_RED;
     const int count = N.count[X];
     N.internal[li] = 0;
     N.left[X] = -1;
@@ -977,6 +988,136 @@ __global__ void k_sah_decide(SahLevel N, int base, int n_lev, const uint32_t* __
     }
     N.nless[X] = l;
     N.internal[li] = 1;
+}
+
+// Small nodes (at most SAH_SMALL items: the deep levels, where almost every node is one) are binned and decided by one
+// thread each, from their items, without the reduction area: k_sah_bounds / k_sah_bins / k_sah_decide then run over
+// the big nodes only, and the area holds big nodes (n / (SAH_SMALL + 1) at most) instead of every node of the level
+// (n_lev x 10.7 KB: 2.7 GB at config E's deepest levels).  The decision is the binned one, candidate for candidate:
+//   * bounds and centroid bounds: the same ord() minima and maxima;
+//   * a split between bins b and b + 1 has the same cost for every b of a run of empty bins, so the strictly-smaller
+//     sweep of k_sah_decide picks the first b of each run, the last non-empty bin on the left: this sweep visits the
+//     non-empty bins only (the items sorted by bin), in the same order, with the same left / right boxes (the same fminf
+//     / fmaxf sequence, empty bins being no-ops) and the same cost expression.
+constexpr int SAH_SMALL = 16;
+
+__global__ void k_sah_small(SahLevel N, int base, int n_lev, const int* __restrict__ big, const uint32_t* __restrict__ perm,
+                            const float* __restrict__ ilo, const float* __restrict__ ihi, const float* __restrict__ ic,
+                            const int* __restrict__ isph, int n, int leaf_size, float trav_cost) {
+    const int li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= n_lev || big[li] >= 0) return;
+    const int X = base + li, count = N.count[X], start = N.start[X];
+    N.internal[li] = 0;
+    N.left[X] = -1;
+    uint32_t t[SAH_SMALL];
+    uint32_t blo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, bhi[3] = {0u, 0u, 0u};
+    uint32_t cmin[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, cmax[3] = {0u, 0u, 0u};
+    int nsp = 0;
+    for (int k = 0; k < count; ++k) {   // k_sah_bounds
+        t[k] = perm[start + k];
+        for (int a = 0; a < 3; ++a) {
+            blo[a] = min(blo[a], ord(ilo[(size_t)a * n + t[k]]));
+            bhi[a] = max(bhi[a], ord(ihi[(size_t)a * n + t[k]]));
+            const uint32_t c = ord(ic[(size_t)a * n + t[k]]);
+            cmin[a] = min(cmin[a], c);
+            cmax[a] = max(cmax[a], c);
+        }
+        nsp += isph[t[k]] != 0;
+    }
+    float lo[3], hi[3], clo[3], sc[3];   // k_sah_prep
+    for (int a = 0; a < 3; ++a) { lo[a] = unord(blo[a]); hi[a] = unord(bhi[a]); }
+    pad_box_dev(lo, hi);
+    for (int a = 0; a < 3; ++a) {
+        N.lo[3 * (size_t)X + a] = lo[a];
+        N.hi[3 * (size_t)X + a] = hi[a];
+        clo[a] = unord(cmin[a]);
+        const float ext = unord(cmax[a]) - clo[a];
+        N.clo[3 * (size_t)X + a] = clo[a];
+        sc[a] = (ext > 0.f && count > 1) ? (float)SAH_BINS / ext : 0.f;
+        N.scale[3 * (size_t)X + a] = sc[a];
+    }
+    if (count <= 1) return;             // k_sah_decide
+    const bool leaf_ok = nsp == 0 && count <= leaf_size;
+    float best_cost = INFINITY;
+    int best_axis = -1, best_split = 0;
+    for (int a = 0; a < 3; ++a) {
+        if (sc[a] == 0.f) continue;
+        int bin[SAH_SMALL], ord_k[SAH_SMALL];
+        for (int k = 0; k < count; ++k) {   // items by bin (insertion sort; equal bins keep item order)
+            bin[k] = sah_bin(ic[(size_t)a * n + t[k]], clo[a], sc[a]);
+            int j = k;
+            while (j > 0 && bin[ord_k[j - 1]] > bin[k]) { ord_k[j] = ord_k[j - 1]; --j; }
+            ord_k[j] = k;
+        }
+        // groups of equal bins: count, box (ord min / max of the items, as the bins hold them)
+        int gb[SAH_SMALL], gc[SAH_SMALL], G = 0;
+        uint32_t glo[SAH_SMALL][3], ghi[SAH_SMALL][3];
+        for (int q = 0; q < count; ++q) {
+            const int k = ord_k[q];
+            if (G == 0 || gb[G - 1] != bin[k]) {
+                gb[G] = bin[k];
+                gc[G] = 0;
+                for (int d = 0; d < 3; ++d) { glo[G][d] = 0xffffffffu; ghi[G][d] = 0u; }
+                ++G;
+            }
+            ++gc[G - 1];
+            for (int d = 0; d < 3; ++d) {
+                glo[G - 1][d] = min(glo[G - 1][d], ord(ilo[(size_t)d * n + t[k]]));
+                ghi[G - 1][d] = max(ghi[G - 1][d], ord(ihi[(size_t)d * n + t[k]]));
+            }
+        }
+        float right_area[SAH_SMALL];
+        int right_cnt[SAH_SMALL];
+        float rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int rc = 0;
+        for (int g = G - 1; g > 0; --g) {   // the bins above the first non-empty one, from the top
+            rc += gc[g];
+            for (int d = 0; d < 3; ++d) { rlo[d] = fminf(rlo[d], unord(glo[g][d])); rhi[d] = fmaxf(rhi[d], unord(ghi[g][d])); }
+            right_cnt[g] = rc;
+            right_area[g] = half_area_dev(rlo, rhi);
+        }
+        float llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int lc = 0;
+        for (int g = 0; g + 1 < G; ++g) {
+            lc += gc[g];
+            for (int d = 0; d < 3; ++d) { llo[d] = fminf(llo[d], unord(glo[g][d])); lhi[d] = fmaxf(lhi[d], unord(ghi[g][d])); }
+            const float cost = half_area_dev(llo, lhi) * lc + right_area[g + 1] * right_cnt[g + 1];
+            if (cost < best_cost) { best_cost = cost; best_axis = a; best_split = gb[g] + 1; }
+        }
+    }
+    const float node_area = fmaxf(half_area_dev(lo, hi), 1e-30f);
+    if (leaf_ok && (best_axis < 0 || trav_cost + best_cost / node_area >= (float)count)) return;
+    N.axis[X] = best_axis;
+    N.split[X] = best_split;
+    int l = count / 2;                            // no usable split: halves (every centroid is the same)
+    if (best_axis >= 0) {
+        l = 0;
+        for (int k = 0; k < count; ++k) l += sah_bin(ic[(size_t)best_axis * n + t[k]], clo[best_axis], sc[best_axis]) < best_split;
+    }
+    N.nless[X] = l;
+    N.internal[li] = 1;
+}
+
+// big[li] = the rank of level node li among the level's nodes of more than SAH_SMALL items, -1 for the others
+// (single workgroup); total[0] = how many
+__global__ __launch_bounds__(1024) void k_big_scan(SahLevel N, int base, int n_lev, int* __restrict__ big,
+                                                   int* __restrict__ total) {
+    __shared__ int part[1024];
+    const int tid = threadIdx.x, per = (n_lev + 1023) / 1024;
+    const int b = min(n_lev, tid * per), e = min(n_lev, b + per);
+    int c = 0;
+    for (int i = b; i < e; ++i) c += N.count[base + i] > SAH_SMALL;
+    part[tid] = c;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int add = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += add;
+        __syncthreads();
+    }
+    int r = part[tid] - c;
+    for (int i = b; i < e; ++i) big[i] = N.count[base + i] > SAH_SMALL ? r++ : -1;
+    if (tid == 1023) total[0] = part[1023];
 }
 
 // ranks of the level's splitting nodes (single workgroup); stats[0] = how many
@@ -1089,6 +1230,8 @@ int crtx_build_sah_gpu(int device, const std::vector<crt_sah::Item>& items, int 
     BTRY(A.alloc(&d_seg2, n));
     BTRY(A.alloc(&d_irank, lev_cap));
     BTRY(A.alloc(&d_stats, 2));
+    int* d_big;
+    BTRY(A.alloc(&d_big, lev_cap));
     SahLevel N;
     BTRY(A.alloc(&N.start, cap));
     BTRY(A.alloc(&N.count, cap));
@@ -1113,16 +1256,28 @@ int crtx_build_sah_gpu(int device, const std::vector<crt_sah::Item>& items, int 
     std::vector<int> level_off = {0, 1};
     for (;;) {
         const int base = level_off[level_off.size() - 2], n_lev = level_off.back() - base;
-        if ((size_t)n_lev * SAH_RED > red_cap) {   // grow the per-level reduction area
-            red_cap = std::max((size_t)n_lev * SAH_RED, 2 * red_cap);
-            BTRY(A.alloc(&d_red, red_cap));
+        hipLaunchKernelGGL(k_big_scan, dim3(1), dim3(1024), 0, st, N, base, n_lev, d_big, d_stats + 1);
+        int n_big = 0;
+        BTRY(hipMemcpyAsync(&n_big, d_stats + 1, 4, hipMemcpyDeviceToHost, st));
+        BTRY(hipStreamSynchronize(st));
+        if (n_big > 0) {
+            if ((size_t)n_big * SAH_RED > red_cap) {   // grow the reduction area (big nodes only)
+                red_cap = std::max((size_t)n_big * SAH_RED, 2 * red_cap);
+                BTRY(A.alloc(&d_red, red_cap));
+            }
+            hipLaunchKernelGGL(k_sah_reset, dim3(blocks((size_t)n_big * SAH_RED)), dim3(256), 0, st, d_red, n_big);
+            const int chunks = (n + SAH_CHUNK - 1) / SAH_CHUNK;
+            hipLaunchKernelGGL(k_sah_bounds, dim3(chunks), dim3(256), 0, st, d_seg, d_perm, d_lo, d_hi, d_c, d_sph, n, d_big,
+                               d_red);
+            hipLaunchKernelGGL(k_sah_prep, dim3(blocks(n_lev)), dim3(256), 0, st, N, base, n_lev, d_big, d_red);
+            hipLaunchKernelGGL(k_sah_bins, dim3(chunks), dim3(256), 0, st, d_seg, d_perm, d_lo, d_hi, d_c, n, N, base, d_big,
+                               d_red);
+            hipLaunchKernelGGL(k_sah_decide, dim3(blocks(n_lev)), dim3(256), 0, st, N, base, n_lev, d_big, d_red, leaf_size,
+                               trav_cost);
         }
-        hipLaunchKernelGGL(k_sah_reset, dim3(blocks((size_t)n_lev * SAH_RED)), dim3(256), 0, st, d_red, n_lev);
-        const int chunks = (n + SAH_CHUNK - 1) / SAH_CHUNK;
-        hipLaunchKernelGGL(k_sah_bounds, dim3(chunks), dim3(256), 0, st, d_seg, d_perm, d_lo, d_hi, d_c, d_sph, n, d_red);
-        hipLaunchKernelGGL(k_sah_prep, dim3(blocks(n_lev)), dim3(256), 0, st, N, base, n_lev, d_red);
-        hipLaunchKernelGGL(k_sah_bins, dim3(chunks), dim3(256), 0, st, d_seg, d_perm, d_lo, d_hi, d_c, n, N, base, d_red);
-        hipLaunchKernelGGL(k_sah_decide, dim3(blocks(n_lev)), dim3(256), 0, st, N, base, n_lev, d_red, leaf_size, trav_cost);
+        if (n_big < n_lev)
+            hipLaunchKernelGGL(k_sah_small, dim3(blocks(n_lev)), dim3(256), 0, st, N, base, n_lev, d_big, d_perm, d_lo, d_hi,
+                               d_c, d_sph, n, leaf_size, trav_cost);
         hipLaunchKernelGGL(k_sah_scan, dim3(1), dim3(1024), 0, st, N, n_lev, d_irank, d_stats);
         int n_int = 0;
         BTRY(hipMemcpyAsync(&n_int, d_stats, 4, hipMemcpyDeviceToHost, st));
