@@ -10,6 +10,8 @@
 #include <thread>
 #include <unordered_map>
 
+#include "ParallelFor.h"
+
 namespace CRT {
 
 static inline bool is_digit(char c) { return c >= '0' && c <= '9'; }
@@ -277,13 +279,9 @@ bool LoadObj(ObjData* out, std::string* err, const char* filename, const char* m
     }
     const auto spans = split_runs(buf);
     std::vector<Run> runs(spans.size());
-    {
-        std::vector<std::thread> th;
-        for (size_t k = 1; k < spans.size(); ++k)
-            th.emplace_back(parse_run, spans[k].first, spans[k].second, &runs[k]);
-        if (!spans.empty()) parse_run(spans[0].first, spans[0].second, &runs[0]);
-        for (auto& x : th) x.join();
-    }
+    parallel_ranges_indexed(spans.size(), [&](size_t, size_t b, size_t e) {
+        for (size_t k = b; k < e; ++k) parse_run(spans[k].first, spans[k].second, &runs[k]);
+    }, 1);
     // join in file order: the usemtl / mtllib lines in sequence (mtllib loads materials that later usemtl lines look up),
     // then each run's vertices and triangles
     std::unordered_map<std::string, int> mat_map;
@@ -318,24 +316,20 @@ bool LoadObj(ObjData* out, std::string* err, const char* filename, const char* m
     out->vertices.resize(n_vert);
     out->triIndices.resize(3 * n_tri);
     out->triMaterial.resize(n_tri);
-    {
-        std::vector<std::thread> th;
-        size_t vb = 0, tb = 0;
-        for (size_t k = 0; k < runs.size(); ++k) {
-            auto fill = [&, k, vb, tb]() {
-                const Run& R = runs[k];
-                std::copy(R.vertices.begin(), R.vertices.end(), out->vertices.begin() + vb);
-                const int32_t vbase = (int32_t)(vb / 3);
-                for (size_t i = 0; i < R.tri.size(); ++i) out->triIndices[3 * tb + i] = R.rel[i] ? vbase + R.tri[i] : R.tri[i];
-                for (size_t i = 0; i < R.tri_event.size(); ++i) out->triMaterial[tb + i] = mat_after[k][R.tri_event[i]];
-            };
-            if (k + 1 < runs.size()) th.emplace_back(fill);
-            else fill();
-            vb += runs[k].vertices.size();
-            tb += runs[k].tri_event.size();
-        }
-        for (auto& x : th) x.join();
+    std::vector<size_t> vb(runs.size() + 1, 0), tb(runs.size() + 1, 0);   // each run's first float / triangle
+    for (size_t k = 0; k < runs.size(); ++k) {
+        vb[k + 1] = vb[k] + runs[k].vertices.size();
+        tb[k + 1] = tb[k] + runs[k].tri_event.size();
     }
+    parallel_ranges_indexed(runs.size(), [&](size_t, size_t b, size_t e) {
+        for (size_t k = b; k < e; ++k) {
+            const Run& R = runs[k];
+            std::copy(R.vertices.begin(), R.vertices.end(), out->vertices.begin() + vb[k]);
+            const int32_t vbase = (int32_t)(vb[k] / 3);
+            for (size_t i = 0; i < R.tri.size(); ++i) out->triIndices[3 * tb[k] + i] = R.rel[i] ? vbase + R.tri[i] : R.tri[i];
+            for (size_t i = 0; i < R.tri_event.size(); ++i) out->triMaterial[tb[k] + i] = mat_after[k][R.tri_event[i]];
+        }
+    }, 1);
     return true;
 }
 

@@ -2,6 +2,7 @@
 #pragma once
 #include <algorithm>
 #include <cstddef>
+#include <exception>
 #include <thread>
 #include <vector>
 
@@ -19,11 +20,27 @@ size_t parallel_ranges_indexed(size_t n, F&& f, size_t min_per_thread = (size_t)
         f((size_t)0, (size_t)0, n);
         return 1;
     }
+    // an exception in a worker (std::bad_alloc) is rethrown here after every worker has joined, as the sequential loop
+    // would have thrown it, instead of terminating the process
+    std::vector<std::exception_ptr> err(T);
     std::vector<std::thread> th;
     th.reserve(T - 1);
-    for (size_t t = 1; t < T; ++t) th.emplace_back([&f, n, T, t]() { f(t, n * t / T, n * (t + 1) / T); });
-    f((size_t)0, (size_t)0, n / T);
+    for (size_t t = 1; t < T; ++t)
+        th.emplace_back([&f, &err, n, T, t]() {
+            try {
+                f(t, n * t / T, n * (t + 1) / T);
+            } catch (...) {
+                err[t] = std::current_exception();
+            }
+        });
+    try {
+        f((size_t)0, (size_t)0, n / T);
+    } catch (...) {
+        err[0] = std::current_exception();
+    }
     for (auto& x : th) x.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
     return T;
 }
 
