@@ -193,15 +193,27 @@ __global__ void k_level_reset(uint32_t* __restrict__ red, int n_lev) {
     red[i] = v;
 }
 
-// Common prologue: the lane's level node (local index) and whether the wave holds a single node.
+// The lane's level node (local index) and whether the wave holds a single node.
 struct LaneSeg {
     int s;          // level-local node index, -1 = not in an internal node of this level
     bool uniform;   // every lane with s >= 0 has the same s (and at least one has)
     int s0;
 };
-__device__ __forceinline__ LaneSeg lane_seg(const int* __restrict__ seg, int p, int n) {
+
+// Steps 2 and 3 run per workgroup chunk of LEVEL_CHUNK positions, and only over the level's big nodes (more than
+// LEVEL_SMALL triangles).  A node's triangles occupy one contiguous range of positions, so a chunk whose first and last
+// positions belong to one node holds that node only (the top levels): it reduces in registers and LDS and adds its
+// result with one global atomic per word, where every wave used to (1M triangles: 16k waves on one node's 48 words).
+// Nodes of at most LEVEL_SMALL triangles (the deep levels) are reduced by one thread each from their triangles
+// (k_level_small), without atomics.  Min, max and add are order-independent: the same words, the same tree.
+constexpr int LEVEL_CHUNK = 4096;
+constexpr int LEVEL_SMALL = 32;
+
+// The lane's big level node (local index) or -1, and whether the wave holds a single one.
+__device__ __forceinline__ LaneSeg lane_seg_big(const int* __restrict__ seg, int p, int n, const Nodes& N, int base) {
     LaneSeg L;
-    L.s = p < n ? seg[p] : -1;
+    const int s = p < n ? seg[p] : -1;
+    L.s = s >= 0 && N.count[base + s] > LEVEL_SMALL ? s : -1;
     const int hi = wave_max_i(L.s);
     const int lo = wave_min_i(L.s >= 0 ? L.s : 0x7fffffff);
     L.uniform = hi >= 0 && lo == hi;
@@ -209,28 +221,73 @@ __device__ __forceinline__ LaneSeg lane_seg(const int* __restrict__ seg, int p, 
     return L;
 }
 
+// block-wide min / max / add of K words per thread into part[K] (thread 0..K-1 then hold the results); op[k]: 0 add,
+// 1 min, 2 max
+template <int K>
+__device__ __forceinline__ uint32_t block_reduce(uint32_t (&v)[K], const int (&op)[K], uint32_t (*part)[K], int k) {
+    const int w = threadIdx.x >> 6;
+    for (int q = 0; q < K; ++q) {
+        uint32_t r = v[q];
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t x = (uint32_t)__shfl_xor((int)r, o, 64);
+            r = op[q] == 0 ? r + x : op[q] == 1 ? min(r, x) : max(r, x);
+        }
+        if ((threadIdx.x & 63) == 0) part[w][q] = r;
+    }
+    __syncthreads();
+    uint32_t r = 0;
+    if (k < K) {
+        r = part[0][k];
+        for (int q = 1; q < 4; ++q) r = op[k] == 0 ? r + part[q][k] : op[k] == 1 ? min(r, part[q][k]) : max(r, part[q][k]);
+    }
+    return r;
+}
+
 // ---- level step 2: centroid bounds per node (Mesh.cuh:164-172) ----
-__global__ void k_level_bounds(const int* __restrict__ seg, const uint32_t* __restrict__ perm,
-                               const float* __restrict__ cen, int n, uint32_t* __restrict__ red) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    const LaneSeg L = lane_seg(seg, p, n);
-    if (L.s0 < 0) return;   // whole wave idle
-    const uint32_t t = L.s >= 0 ? perm[p] : 0;
-    uint32_t c[3];
-    for (int a = 0; a < 3; ++a) c[a] = L.s >= 0 ? ord(cen[(size_t)a * n + t]) : 0;
-    if (L.uniform) {
-        for (int a = 0; a < 3; ++a) {
-            const uint32_t mn = wave_min(L.s >= 0 ? c[a] : 0xffffffffu);
-            const uint32_t mx = wave_max(L.s >= 0 ? c[a] : 0u);
-            if ((threadIdx.x & 63) == 0) {
-                atomicMin(&red[L.s0 * RED + a], mn);
-                atomicMax(&red[L.s0 * RED + 3 + a], mx);
+__global__ __launch_bounds__(256) void k_level_bounds(const int* __restrict__ seg, const uint32_t* __restrict__ perm,
+                                                      const float* __restrict__ cen, int n, Nodes N, int base,
+                                                      uint32_t* __restrict__ red) {
+    __shared__ uint32_t part[4][6];
+    const int p0 = blockIdx.x * LEVEL_CHUNK, p1 = min(n, p0 + LEVEL_CHUNK);
+    const int s_first = seg[p0];
+    if (s_first >= 0 && seg[p1 - 1] == s_first && N.count[base + s_first] > LEVEL_SMALL) {   // one big node
+        uint32_t v[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+        const int op[6] = {1, 1, 1, 2, 2, 2};
+        for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {
+            const uint32_t t = perm[p];
+            for (int a = 0; a < 3; ++a) {
+                const uint32_t c = ord(cen[(size_t)a * n + t]);
+                v[a] = min(v[a], c);
+                v[3 + a] = max(v[3 + a], c);
             }
         }
-    } else if (L.s >= 0) {
-        for (int a = 0; a < 3; ++a) {
-            atomicMin(&red[L.s * RED + a], c[a]);
-            atomicMax(&red[L.s * RED + 3 + a], c[a]);
+        const int k = threadIdx.x;
+        const uint32_t r = block_reduce<6>(v, op, part, k);
+        if (k < 3) atomicMin(&red[s_first * RED + k], r);
+        else if (k < 6) atomicMax(&red[s_first * RED + k], r);
+        return;
+    }
+    for (int q = p0; q < p1; q += 256) {
+        const int p = q + (int)threadIdx.x;
+        const LaneSeg L = lane_seg_big(seg, p, p1, N, base);
+        if (L.s0 < 0) continue;   // whole wave idle
+        const uint32_t t = L.s >= 0 ? perm[p] : 0;
+        uint32_t c[3];
+        for (int a = 0; a < 3; ++a) c[a] = L.s >= 0 ? ord(cen[(size_t)a * n + t]) : 0;
+        if (L.uniform) {
+            for (int a = 0; a < 3; ++a) {
+                const uint32_t mn = wave_min(L.s >= 0 ? c[a] : 0xffffffffu);
+                const uint32_t mx = wave_max(L.s >= 0 ? c[a] : 0u);
+                if ((threadIdx.x & 63) == 0) {
+                    atomicMin(&red[L.s0 * RED + a], mn);
+                    atomicMax(&red[L.s0 * RED + 3 + a], mx);
+                }
+            }
+        } else if (L.s >= 0) {
+            for (int a = 0; a < 3; ++a) {
+                atomicMin(&red[L.s * RED + a], c[a]);
+                atomicMax(&red[L.s * RED + 3 + a], c[a]);
+            }
         }
     }
 }
@@ -240,44 +297,129 @@ __device__ __forceinline__ float node_mid(const uint32_t* __restrict__ r, int a)
 }
 
 // ---- level step 3: SAH side counts and boxes for the three candidate splits (evaluateSAH) ----
-__global__ void k_level_sah(const int* __restrict__ seg, const uint32_t* __restrict__ perm,
-                            const float* __restrict__ cen, const float* __restrict__ tlo,
-                            const float* __restrict__ thi, int n, uint32_t* __restrict__ red) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    const LaneSeg L = lane_seg(seg, p, n);
-    if (L.s0 < 0) return;
-    const bool act = L.s >= 0;
-    const uint32_t t = act ? perm[p] : 0;
-    const int me = act ? L.s : L.s0;
-    uint32_t lo[3], hi[3];
-    for (int a = 0; a < 3; ++a) {
-        lo[a] = act ? ord(tlo[(size_t)a * n + t]) : 0xffffffffu;
-        hi[a] = act ? ord(thi[(size_t)a * n + t]) : 0u;
-    }
-    for (int a = 0; a < 3; ++a) {
-        const float mid = node_mid(red + (size_t)me * RED, a);
-        const int side = act ? (cen[(size_t)a * n + t] < mid ? 0 : 1) : -1;   // 0 = left (c[axis] < pos)
-        if (L.uniform) {
-            for (int sd = 0; sd < 2; ++sd) {
-                const bool in = side == sd;
-                const uint64_t bal = __ballot(in);
-                if (!bal) continue;
-                uint32_t r[6];
-                for (int k = 0; k < 3; ++k) {
-                    r[k] = wave_min(in ? lo[k] : 0xffffffffu);
-                    r[3 + k] = wave_max(in ? hi[k] : 0u);
-                }
-                if ((threadIdx.x & 63) == 0) {
-                    uint32_t* o = red + (size_t)L.s0 * RED + 6 + (a * 2 + sd) * 7;
-                    atomicAdd(&o[0], (uint32_t)__popcll(bal));
-                    for (int k = 0; k < 3; ++k) { atomicMin(&o[1 + k], r[k]); atomicMax(&o[4 + k], r[3 + k]); }
+__global__ __launch_bounds__(256) void k_level_sah(const int* __restrict__ seg, const uint32_t* __restrict__ perm,
+                                                   const float* __restrict__ cen, const float* __restrict__ tlo,
+                                                   const float* __restrict__ thi, int n, Nodes N, int base,
+                                                   uint32_t* __restrict__ red) {
+    __shared__ uint32_t part[4][42];
+    const int p0 = blockIdx.x * LEVEL_CHUNK, p1 = min(n, p0 + LEVEL_CHUNK);
+    const int s_first = seg[p0];
+    if (s_first >= 0 && seg[p1 - 1] == s_first && N.count[base + s_first] > LEVEL_SMALL) {   // one big node
+        uint32_t v[42];   // per axis and side: count, lo[3], hi[3]
+        int op[42];
+        for (int q = 0; q < 42; ++q) {
+            const int k = q % 7;
+            v[q] = k == 0 ? 0u : k < 4 ? 0xffffffffu : 0u;
+            op[q] = k == 0 ? 0 : k < 4 ? 1 : 2;
+        }
+        float mid[3];
+        for (int a = 0; a < 3; ++a) mid[a] = node_mid(red + (size_t)s_first * RED, a);
+        for (int p = p0 + (int)threadIdx.x; p < p1; p += 256) {
+            const uint32_t t = perm[p];
+            uint32_t lo[3], hi[3];
+            for (int k = 0; k < 3; ++k) { lo[k] = ord(tlo[(size_t)k * n + t]); hi[k] = ord(thi[(size_t)k * n + t]); }
+            for (int a = 0; a < 3; ++a) {
+                const int side = cen[(size_t)a * n + t] < mid[a] ? 0 : 1;   // 0 = left (c[axis] < pos)
+                for (int sd = 0; sd < 2; ++sd) {   // unrolled selects: v stays in registers
+                    uint32_t* o = v + (a * 2 + sd) * 7;
+                    const bool in = side == sd;
+                    o[0] += in ? 1u : 0u;
+                    for (int k = 0; k < 3; ++k) {
+                        o[1 + k] = in ? min(o[1 + k], lo[k]) : o[1 + k];
+                        o[4 + k] = in ? max(o[4 + k], hi[k]) : o[4 + k];
+                    }
                 }
             }
-        } else if (act) {
-            uint32_t* o = red + (size_t)L.s * RED + 6 + (a * 2 + side) * 7;
-            atomicAdd(&o[0], 1u);
-            for (int k = 0; k < 3; ++k) { atomicMin(&o[1 + k], lo[k]); atomicMax(&o[4 + k], hi[k]); }
         }
+        const int k = threadIdx.x;
+        const uint32_t r = block_reduce<42>(v, op, part, k);
+        if (k < 42) {
+            uint32_t* o = red + (size_t)s_first * RED + 6 + k;
+            const int w = k % 7;
+            if (w == 0) { if (r) atomicAdd(o, r); }
+            else if (w < 4) atomicMin(o, r);
+            else atomicMax(o, r);
+        }
+        return;
+    }
+    for (int q = p0; q < p1; q += 256) {
+        const int p = q + (int)threadIdx.x;
+        const LaneSeg L = lane_seg_big(seg, p, p1, N, base);
+        if (L.s0 < 0) continue;
+        const bool act = L.s >= 0;
+        const uint32_t t = act ? perm[p] : 0;
+        const int me = act ? L.s : L.s0;
+        uint32_t lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = act ? ord(tlo[(size_t)a * n + t]) : 0xffffffffu;
+            hi[a] = act ? ord(thi[(size_t)a * n + t]) : 0u;
+        }
+        for (int a = 0; a < 3; ++a) {
+            const float mid = node_mid(red + (size_t)me * RED, a);
+            const int side = act ? (cen[(size_t)a * n + t] < mid ? 0 : 1) : -1;   // 0 = left (c[axis] < pos)
+            if (L.uniform) {
+                for (int sd = 0; sd < 2; ++sd) {
+                    const bool in = side == sd;
+                    const uint64_t bal = __ballot(in);
+                    if (!bal) continue;
+                    uint32_t r[6];
+                    for (int k = 0; k < 3; ++k) {
+                        r[k] = wave_min(in ? lo[k] : 0xffffffffu);
+                        r[3 + k] = wave_max(in ? hi[k] : 0u);
+                    }
+                    if ((threadIdx.x & 63) == 0) {
+                        uint32_t* o = red + (size_t)L.s0 * RED + 6 + (a * 2 + sd) * 7;
+                        atomicAdd(&o[0], (uint32_t)__popcll(bal));
+                        for (int k = 0; k < 3; ++k) { atomicMin(&o[1 + k], r[k]); atomicMax(&o[4 + k], r[3 + k]); }
+                    }
+                }
+            } else if (act) {
+                uint32_t* o = red + (size_t)L.s * RED + 6 + (a * 2 + side) * 7;
+                atomicAdd(&o[0], 1u);
+                for (int k = 0; k < 3; ++k) { atomicMin(&o[1 + k], lo[k]); atomicMax(&o[4 + k], hi[k]); }
+            }
+        }
+    }
+}
+
+// Steps 2 and 3 for the level's small internal nodes (LEVEL_SMALL triangles or fewer), one thread each: the words the
+// atomics of k_level_bounds / k_level_sah would leave, from the reset values (k_level_reset) and the same ord() minima,
+// maxima and counts.
+__global__ void k_level_small(Nodes N, int base, int n_lev, const int* __restrict__ irank, const uint32_t* __restrict__ perm,
+                              const float* __restrict__ cen, const float* __restrict__ tlo, const float* __restrict__ thi,
+                              int n, uint32_t* __restrict__ red) {
+    const int li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= n_lev || irank[li] < 0) return;
+    const int X = base + li, count = N.count[X], start = N.start[X];
+    if (count > LEVEL_SMALL) return;
+    uint32_t* r = red + (size_t)li * RED;
+    uint32_t cmin[3], cmax[3];
+    for (int a = 0; a < 3; ++a) { cmin[a] = r[a]; cmax[a] = r[3 + a]; }   // ord(1e30f), ord(-1e30f)
+    for (int k = 0; k < count; ++k) {
+        const uint32_t t = perm[start + k];
+        for (int a = 0; a < 3; ++a) {
+            const uint32_t c = ord(cen[(size_t)a * n + t]);
+            cmin[a] = min(cmin[a], c);
+            cmax[a] = max(cmax[a], c);
+        }
+    }
+    for (int a = 0; a < 3; ++a) { r[a] = cmin[a]; r[3 + a] = cmax[a]; }
+    for (int a = 0; a < 3; ++a) {
+        const float mid = node_mid(r, a);
+        uint32_t o[2][7];
+        for (int sd = 0; sd < 2; ++sd)
+            for (int k = 0; k < 7; ++k) o[sd][k] = r[6 + (a * 2 + sd) * 7 + k];
+        for (int k = 0; k < count; ++k) {
+            const uint32_t t = perm[start + k];
+            const int sd = cen[(size_t)a * n + t] < mid ? 0 : 1;
+            o[sd][0] += 1u;
+            for (int q = 0; q < 3; ++q) {
+                o[sd][1 + q] = min(o[sd][1 + q], ord(tlo[(size_t)q * n + t]));
+                o[sd][4 + q] = max(o[sd][4 + q], ord(thi[(size_t)q * n + t]));
+            }
+        }
+        for (int sd = 0; sd < 2; ++sd)
+            for (int k = 0; k < 7; ++k) r[6 + (a * 2 + sd) * 7 + k] = o[sd][k];
     }
 }
 
@@ -643,8 +785,12 @@ extern "C" int crt_build_mesh_bvh(int device, const float* positions, uint32_t v
         if (n_int == 0 || err) break;   // done, or a degenerate split / bad index: reported below
         const int next_base = level_off.back();
         hipLaunchKernelGGL(k_level_reset, dim3(blocks((size_t)n_lev * RED)), dim3(256), 0, st, d_red, n_lev);
-        hipLaunchKernelGGL(k_level_bounds, dim3(blocks(n)), dim3(256), 0, st, d_seg, d_perm, d_cen, n, d_red);
-        hipLaunchKernelGGL(k_level_sah, dim3(blocks(n)), dim3(256), 0, st, d_seg, d_perm, d_cen, d_tlo, d_thi, n, d_red);
+        const int lchunks = (n + LEVEL_CHUNK - 1) / LEVEL_CHUNK;
+        hipLaunchKernelGGL(k_level_bounds, dim3(lchunks), dim3(256), 0, st, d_seg, d_perm, d_cen, n, N, base, d_red);
+        hipLaunchKernelGGL(k_level_sah, dim3(lchunks), dim3(256), 0, st, d_seg, d_perm, d_cen, d_tlo, d_thi, n, N, base,
+                           d_red);
+        hipLaunchKernelGGL(k_level_small, dim3(blocks(n_lev)), dim3(256), 0, st, N, base, n_lev, d_irank, d_perm, d_cen,
+                           d_tlo, d_thi, n, d_red);
         hipLaunchKernelGGL(k_level_decide, dim3(blocks(n_lev)), dim3(256), 0, st, N, base, n_lev, d_irank, d_red,
                            next_base, d_err);
         hipLaunchKernelGGL(k_level_flags, dim3(blocks(n)), dim3(256), 0, st, d_seg, d_perm, d_cen, n, N, base, d_flags);
