@@ -2,7 +2,10 @@
 (the library reads the variable per render), on configs B / C / E.  Frames, RNG state and ray counts must not depend
 on it.
 
-    python tools/help_ab.py [--configs B,C] [--values 0,-1,1024] [--reps 3]
+    git apply profiles/r05y/helpers.patch && make -C raytracer-cuda_amd all
+    python tools/help_ab.py [--configs B,C] [--values 0,-1,1024] [--reps 3] [--parity]
+
+Measured and not kept (profiles/r05y): without the patch the library ignores CRT_HELPER_TILES.
 """
 import argparse
 import hashlib
