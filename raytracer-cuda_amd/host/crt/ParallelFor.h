@@ -23,21 +23,24 @@ size_t parallel_ranges_indexed(size_t n, F&& f, size_t min_per_thread = (size_t)
     // an exception in a worker (std::bad_alloc) is rethrown here after every worker has joined, as the sequential loop
     // would have thrown it, instead of terminating the process
     std::vector<std::exception_ptr> err(T);
+    auto run = [&f, &err, n, T](size_t t) {
+        try {
+            f(t, n * t / T, n * (t + 1) / T);
+        } catch (...) {
+            err[t] = std::current_exception();
+        }
+    };
     std::vector<std::thread> th;
     th.reserve(T - 1);
-    for (size_t t = 1; t < T; ++t)
-        th.emplace_back([&f, &err, n, T, t]() {
-            try {
-                f(t, n * t / T, n * (t + 1) / T);
-            } catch (...) {
-                err[t] = std::current_exception();
-            }
-        });
+    size_t started = 1;   // ranges 1 .. started-1 have a thread
     try {
-        f((size_t)0, (size_t)0, n / T);
+        for (; started < T; ++started) th.emplace_back(run, started);
     } catch (...) {
-        err[0] = std::current_exception();
+        // no thread could be started (std::system_error): the ranges without one run on this thread, after the
+        // others, so no started thread is left unjoined
     }
+    run(0);
+    for (size_t t = started; t < T; ++t) run(t);
     for (auto& x : th) x.join();
     for (auto& e : err)
         if (e) std::rethrow_exception(e);
