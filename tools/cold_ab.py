@@ -21,6 +21,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--configs", default="C")
 ap.add_argument("--occupancy", default="7,8")
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--trees", default="sah", help="comma list of sah / sbvh (spatial splits): interleaved like the occupancies")
 a = ap.parse_args()
 occs = [int(v) for v in a.occupancy.split(",")]
 
@@ -37,20 +38,23 @@ for cfg in a.configs.split(","):
     name, W, H, spp = CONFIGS[cfg]
     if name not in scenes:
         hs = crt_amd.HostScene(assets.scene_files(name), build_device=0)
-        scenes[name] = (hs, hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True))
-    sc = scenes[name][1]
+        scenes[name] = {tr: hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0,
+                                      gpu_build=(tr == "sah"), spatial_splits=(tr == "sbvh"))
+                        for tr in a.trees.split(",")}
+    trees = scenes[name]
     r = crt_amd.Renderer(W, H)
     r.set_kernel_variant(8)
     r.set_camera(crt_amd.camera(spp))
     hashes = {}
+    settings = [(oc, tr) for oc in occs for tr in trees]
     for rep in range(a.reps + 1):
-        for oc in (occs if rep % 2 == 0 else occs[::-1]):
+        for oc, tr in (settings if rep % 2 == 0 else settings[::-1]):
             r.set_occupancy_target(oc)
             r.init_rand(41)
-            r.render(sc, spp, 20)
+            r.render(trees[tr], spp, 20)
             r.synchronize()
             ph = r.last_timings()
-            hashes.setdefault(oc, frame_hash(r))
-            print(json.dumps({"config": cfg, "rep": rep, "occ": oc, "kernel": r.last_kernel_name(),
+            hashes.setdefault(f"{oc}/{tr}", frame_hash(r))
+            print(json.dumps({"config": cfg, "rep": rep, "occ": oc, "tree": tr, "kernel": r.last_kernel_name(),
                               "main_kernel_ms": round(ph["main_kernel_ms"], 3), "rays": r.counters()["rays"]}), flush=True)
     print(json.dumps({"config": cfg, "hashes": {str(k): v for k, v in hashes.items()}}), flush=True)
