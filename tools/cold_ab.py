@@ -21,6 +21,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--configs", default="C")
 ap.add_argument("--occupancy", default="7,8")
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--top-levels", default="-1", help="comma list for crt_renderer_set_top_levels, interleaved too")
 ap.add_argument("--trees", default="sah", help="comma list of sah / sbvh (spatial splits): interleaved like the occupancies")
 a = ap.parse_args()
 occs = [int(v) for v in a.occupancy.split(",")]
@@ -46,15 +47,16 @@ for cfg in a.configs.split(","):
     r.set_kernel_variant(8)
     r.set_camera(crt_amd.camera(spp))
     hashes = {}
-    settings = [(oc, tr) for oc in occs for tr in trees]
+    settings = [(oc, tr, tl) for oc in occs for tr in trees for tl in (int(v) for v in a.top_levels.split(","))]
     for rep in range(a.reps + 1):
-        for oc, tr in (settings if rep % 2 == 0 else settings[::-1]):
+        for oc, tr, tl in (settings if rep % 2 == 0 else settings[::-1]):
             r.set_occupancy_target(oc)
+            r.set_top_levels(tl)
             r.init_rand(41)
             r.render(trees[tr], spp, 20)
             r.synchronize()
             ph = r.last_timings()
-            hashes.setdefault(f"{oc}/{tr}", frame_hash(r))
-            print(json.dumps({"config": cfg, "rep": rep, "occ": oc, "tree": tr, "kernel": r.last_kernel_name(),
+            hashes.setdefault(f"{oc}/{tr}/{tl}", frame_hash(r))
+            print(json.dumps({"config": cfg, "rep": rep, "occ": oc, "tree": tr, "top": tl, "kernel": r.last_kernel_name(),
                               "main_kernel_ms": round(ph["main_kernel_ms"], 3), "rays": r.counters()["rays"]}), flush=True)
     print(json.dumps({"config": cfg, "hashes": {str(k): v for k, v in hashes.items()}}), flush=True)
