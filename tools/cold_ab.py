@@ -16,7 +16,8 @@ import crt_amd  # noqa: E402
 from crt_amd import assets  # noqa: E402
 
 CONFIGS = {"B": ("cornell_bunny", 1280, 720, 256), "C": ("cornell_bunny", 2560, 1440, 2000),
-           "E": ("cornell_1m", 2560, 1440, 512), "S": ("cornell_bunny", 640, 360, 64)}
+           "E": ("cornell_1m", 2560, 1440, 512), "S": ("cornell_bunny", 640, 360, 64),
+           "M": ("cornell_bunny", 1600, 900, 256)}
 ap = argparse.ArgumentParser()
 ap.add_argument("--configs", default="C")
 ap.add_argument("--occupancy", default="7,8")
