@@ -17,13 +17,21 @@ times the bit-exact reference-BVH path itself.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+`--gpus N > 1` without a launcher environment starts `torch.distributed.run --nproc-per-node N` itself, as a child
+process, before anything imports torch or touches a GPU, relays rank 0's JSON line and exits with the child's code; a
+launcher whose WORLD_SIZE differs from --gpus is an error (exit 2).  At N > 1 the line carries each rank's render and
+collective times, the roofline of rank 0's share and a statistical parity field against the 1-GPU frame.
+
 rank 0 prints ONE JSON line (last line of stdout); progress goes to stderr.
 """
 from __future__ import annotations
 
 import argparse
+import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -76,7 +84,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -133,7 +141,15 @@ def parse():
     ap.add_argument("--host-build", action="store_true",
                     help="build the BVHs on the host (mesh: the sequential restatement of the reference builder; "
                          "rebuilt tree: crt_sah.h) instead of on the GPU")
-    args = ap.parse_args()
+    ap.add_argument("--share", type=int, nargs=2, metavar=("G", "N"), default=None,
+                    help="one GPU renders rank G's share of an N-way spp-sharded frame (shard_spp samples from "
+                         "subsequence family G*W*H, no collective): the per-rank workload of the N-GPU line, for PMC "
+                         "passes (tools/pmc.sh) and per-rank costs")
+    ap.add_argument("--rig", default="crt_amd",
+                    help="module providing crt_amd's renderer API (default: crt_amd, the HIP library).  Test hook: "
+                         "tests/helpers/cpu_rig.py rehearses the launch, shard and collective path on CPU; its line is "
+                         "marked 'rehearsal' and measures nothing")
+    args = ap.parse_args(argv)
     # flag combinations the library would reject only at the first render, after the GPU is initialised
     if args.shard == "pixels" and (args.bvh != "rebuilt" or args.bvh_width != 4):
         ap.error("--shard pixels needs the 4-wide rebuilt BVH (--bvh rebuilt --bvh-width 4): it runs variant 8")
@@ -141,7 +157,53 @@ def parse():
         ap.error("--spatial-splits builds the rebuilt tree; it has no effect with --bvh reference")
     if args.bvh_width not in (2, 4):
         ap.error("--bvh-width must be 2 or 4")
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.share is not None:
+        g, n = args.share
+        if not 0 <= g < n or args.gpus != 1 or args.shard != "spp":
+            ap.error("--share G N: 0 <= G < N, one GPU (--gpus 1), spp sharding")
     return args
+
+
+def launched_by_torchrun() -> bool:
+    return "TORCHELASTIC_RUN_ID" in os.environ or all(
+        k in os.environ for k in ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE"))
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args, argv) -> int:
+    """`--gpus N > 1` from a plain `python bench.py`: run the N ranks under torch.distributed.run as a CHILD process
+    (this process has not imported torch, let alone touched a GPU), pass their progress through, print rank 0's JSON
+    line last and return the child's exit code (1 if it succeeded without a line)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve()), *argv]
+    log(f"[launch] --gpus {args.gpus} without a launcher: {' '.join(cmd)}")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    line = None
+    for ln in p.stdout:
+        s = ln.strip()
+        if s.startswith("{"):
+            try:
+                if "metric" in json.loads(s):
+                    line = s
+                    continue
+            except ValueError:
+                pass
+        sys.stdout.write(ln)
+        sys.stdout.flush()
+    rc = p.wait()
+    if line is not None:
+        print(line, flush=True)
+    elif rc == 0:
+        log("[launch] the ranks exited 0 without a JSON line")
+        rc = 1
+    return rc
 
 
 def cgroup_cpu_quota():
@@ -238,13 +300,21 @@ def kernel_source_sha() -> str:
     return hashlib.sha256((REPO / "raytracer-cuda_amd" / "csrc" / "crt_hip.hip").read_bytes()).hexdigest()
 
 
-def roofline_counters(key: str, kname: str):
-    """The committed PMC summary of this workload (tools/pmc_summary.py), if its kernel matches."""
+def roofline_counters(key: str, kname: str, fallback_key: str | None = None):
+    """The committed PMC summary of this workload (tools/pmc_summary.py), if its kernel matches: (entry, rule).
+
+    A rank's share of an N-way frame (fewer spp, other RNG subsequences, same scene, camera and kernel) without a
+    summary of its own takes the per-ray counter values of the whole frame's summary (`fallback_key`), scaled by the
+    share's exact ray count and its own kernel time: rule "per_ray_of:<key>"."""
     p = REPO / "profiles" / "roofline_counters.json"
     if not p.exists():
-        return None
-    e = json.loads(p.read_text()).get(key)
-    return e if e and e.get("kernel") == kname else None
+        return None, None
+    table = json.loads(p.read_text())
+    for k, rule in ((key, "own"), (fallback_key, f"per_ray_of:{fallback_key}")):
+        e = table.get(k) if k else None
+        if e and e.get("kernel") == kname:
+            return e, rule
+    return None, None
 
 
 def roofline_from_counters(e, rays: int, kernel_s: float, algorithmic_ops: int | None = None,
@@ -301,31 +371,55 @@ def roofline_from_counters(e, rays: int, kernel_s: float, algorithmic_ops: int |
             "counters_kernel_source_current": e.get("kernel_source_sha256") == kernel_source_sha()}
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
     if args.print_workload_key:
-        print(workload_key(args, args.spp))
-        return
+        print(workload_key(args, args.spp if args.share is None else shard_spp_of(args)))
+        return 0
+    # the launch decision comes before torch is imported: nothing in this process touches a GPU before the ranks start
+    if launched_by_torchrun():
+        env_world = int(os.environ.get("WORLD_SIZE", "1"))
+        if env_world != args.gpus:
+            log(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
+            return 2
+    elif args.gpus > 1:
+        return spawn_ranks(args, argv)
+    return run(args)
+
+
+def shard_spp_of(args) -> int:
+    g, n = args.share
+    base, rem = divmod(args.spp, n)
+    return base + (1 if g < rem else 0)
+
+
+def run(args) -> int:
     import torch
     import torch.distributed as dist
 
-    import crt_amd
+    crt = importlib.import_module(args.rig)
+    rehearsal = args.rig != "crt_amd"
     from crt_amd import assets
     from crt_amd.dist import ShardedFrameRenderer, dist_env, gather_frame_timings
 
     rank, local, world = dist_env()
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    local = local % max(1, torch.cuda.device_count())   # rehearsal: several ranks may share one GPU (gloo)
-    torch.cuda.set_device(local)
+    on_gpu = getattr(crt, "DEVICE_TYPE", "cuda") == "cuda"
+    if on_gpu:
+        ngpu = torch.cuda.device_count()
+        if args.dist_backend == "nccl" and world > ngpu:
+            log(f"error: {world} ranks over RCCL need {world} GPUs, {ngpu} visible (gloo rehearses N ranks on one GPU)")
+            return 2
+        local = local % max(1, ngpu)   # gloo rehearsal: several ranks may share one GPU
+        torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}" if on_gpu else "cpu")
+    sync = torch.cuda.synchronize if on_gpu else (lambda *a: None)
     # a process group whenever torch.distributed.run launched us, even with one rank: `--nproc-per-node 1` then runs
     # the production collective path (RCCL reduce of the framebuffer on a one-rank communicator) on a single GPU
-    launched = "TORCHELASTIC_RUN_ID" in os.environ or all(
-        k in os.environ for k in ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE"))
-    grouped = world > 1 or launched
+    grouped = world > 1 or launched_by_torchrun()
     if grouped:
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+            dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
         log(f"[dist] rank {rank}/{world}: backend {dist.get_backend()}")
@@ -333,8 +427,8 @@ def main():
     # the HIP runtime's start-up (device context, torch's allocator) is a once-per-process cost that comes before any
     # scene or frame: timed apart (runtime_init_s), so that end_to_end_s is the scene's set-up plus one frame
     t = time.perf_counter()
-    torch.zeros(1, device=f"cuda:{local}")
-    torch.cuda.synchronize()
+    torch.zeros(1, device=dev)
+    sync()
     t_runtime = time.perf_counter() - t
 
     def barrier():
@@ -344,14 +438,14 @@ def main():
     def allreduce_max(x: float) -> float:
         if not grouped:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     def allreduce_sum_i(xs):
         if not grouped:
             return list(xs)
-        t = torch.tensor(list(xs), dtype=torch.int64, device=f"cuda:{local}")
+        t = torch.tensor(list(xs), dtype=torch.int64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return [int(v) for v in t.tolist()]
 
@@ -360,7 +454,7 @@ def main():
     barrier()
     files = assets.scene_files(args.scene)
     t = time.perf_counter()
-    hs = crt_amd.HostScene(files, build_device=None if args.host_build else local)
+    hs = crt.HostScene(files, build_device=None if args.host_build else local)
     t_load = time.perf_counter() - t
     ref_scene = hs.upload(local) if args.bvh != "rebuilt" else None
     scene = ref_scene
@@ -384,10 +478,10 @@ def main():
     log_r(f"[scene] {args.scene}: {counts['n_indices'] // 3} triangles, {st['device_nodes']} nodes, "
           f"{st['device_bytes'] / 1e6:.1f} MB in HBM, load+build+upload {t_scene:.2f}s {setup}")
 
-    cam = crt_amd.camera(args.spp)
+    cam = crt.camera(args.spp)
 
     def make_renderer():
-        rr = crt_amd.Renderer(W, H, local)
+        rr = crt.Renderer(W, H, local)
         if args.kernel_variant is not None:
             rr.set_kernel_variant(args.kernel_variant)
         if args.regen_threshold is not None:
@@ -408,29 +502,44 @@ def main():
         return rr
 
     r = make_renderer()
-    fr = ShardedFrameRenderer(r, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard,
-                              collective=grouped)
-    log_r(f"[plan] {world} rank(s), spp per rank {[fr.spp] if world == 1 else 'spp/N'}")
+    marks = max(64, args.steps + args.warmup)
+
+    def make_frame(rr):
+        if args.share is not None:      # rank G's share of an N-way frame, alone on this GPU
+            g, n = args.share
+            return ShardedFrameRenderer(rr, scene, args.spp, args.bounces, args.seed, g, n, collective=False,
+                                        local_share=True, fb_device=str(dev), max_marks=marks)
+        return ShardedFrameRenderer(rr, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard,
+                                    collective=grouped, fb_device=str(dev), max_marks=marks)
+
+    fr = make_frame(r)
+    log_r(f"[plan] {world} rank(s), spp per rank {[fr.spp] if world == 1 else 'spp/N'}"
+          + (f"; share {args.share[0]} of {args.share[1]}: {fr.spp} spp from subsequence {fr.subseq}"
+             if args.share else ""))
 
     for i in range(args.warmup):
         t = time.perf_counter()
         fr.render()
-        torch.cuda.synchronize()
+        sync()
         log_r(f"[warmup {i}] {time.perf_counter() - t:.3f}s")
 
     fr.reset_timings()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
         fr.render()
-    torch.cuda.synchronize()
+    sync()
     barrier()
     elapsed = time.perf_counter() - t0
     elapsed = allreduce_max(elapsed)
     # per frame: this rank's render (RNG reset excluded; probe, sort and main kernel) and its collective, HIP events on
     # the launch stream; gathered over ranks (a collective: every rank calls it)
     frame_t = fr.frame_timings()
+    assert len(frame_t) == args.steps, f"{len(frame_t)} frame timings for {args.steps} timed frames"
+    # the reduced N-rank frame (rank 0 holds it) before any later launch reuses the framebuffer: the statistical parity
+    # field compares it with the 1-GPU frame
+    lin_frame = fr.linear() if rank == 0 and world > 1 and not args.no_parity else None
     kernel_ms = [f[0] for f in frame_t]
     kernel_ms_avg = sum(kernel_ms) / len(kernel_ms)
     kernel_ms_max = allreduce_max(max(kernel_ms))
@@ -455,15 +564,14 @@ def main():
     # curand_init, no cached state), one frame with the collective and the resolve, and the RGBA8 D2H readback on
     # rank 0, max over ranks
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t = time.perf_counter()
     r_e2e = make_renderer()
-    fr_e2e = ShardedFrameRenderer(r_e2e, scene, args.spp, args.bounces, args.seed, rank, world, mode=args.shard,
-                                  collective=grouped)
+    fr_e2e = make_frame(r_e2e)
     fr_e2e.render()
     if rank == 0:
         r_e2e.rgba8()
-    torch.cuda.synchronize()
+    sync()
     t_frame_e2e = allreduce_max(time.perf_counter() - t)
     t_rb = time.perf_counter()
     if rank == 0:
@@ -523,14 +631,16 @@ def main():
                        "note": "32*box + 36*tri + 20*sphere + 16*ray + 60*pixel bytes; 24*box + 54*tri + 30*sphere "
                                "+ 100*ray f32 ops (DESIGN.md §5); the %.1f MB scene is L2/Infinity-Cache resident"
                                % (st["device_bytes"] / 1e6)}
-    ec = roofline_counters(workload_key(args, fr.spp), kname)
+    ec, ec_rule = roofline_counters(workload_key(args, fr.spp), kname, workload_key(args, args.spp))
     if ec is not None:
         # the counters are the main render kernel's alone, so they are divided by its own time (HIP events around that
         # launch only), not by the whole render's, which includes the cost probe and the tile sort
         roofline = roofline_from_counters(ec, rays_rank, phases_avg["main_kernel_ms"] / 1e3,
                                           algorithmic["ops_per_launch"] if algorithmic else None,
                                           algorithmic["survey_ops_per_launch"] if algorithmic else None)
-        roofline.update(kernel=kname, kernel_ms=round(phases_avg["main_kernel_ms"], 3),
+        roofline.update(kernel=kname, kernel_ms=round(phases_avg["main_kernel_ms"], 3), counters_rule=ec_rule,
+                        workload=f"rank 0's share: {fr.spp} of {args.spp} spp, subsequence {fr.subseq}"
+                        if fr.spp != args.spp else "the whole frame",
                         kernel_ms_note=f"HIP events around the main render launch, average of the {len(hist)} timed "
                                        "frames (probe and tile sort excluded)")
     else:
@@ -550,7 +660,7 @@ def main():
         ref_ms = r.last_kernel_ms()
         ref_rays = r.counters()["rays"]
         lin_ref = r.linear()
-        scale = crt_amd.pixel_sample_scale(args.spp)
+        scale = crt.pixel_sample_scale(args.spp)
         d = ((lin - lin_ref) * scale).astype(np.float64).reshape(-1, 3)
         rms = [float(v) for v in np.sqrt(np.mean(d * d, axis=0))]
         eq = float(np.mean(np.all(lin.view(np.uint32) == lin_ref.view(np.uint32), axis=-1)))
@@ -566,9 +676,13 @@ def main():
         r.resolve(scale)
         r.synchronize()
 
+    if lin_frame is not None:
+        parity = statistical_parity(lin_frame, rays_frame, r, scene, args, world, crt.pixel_sample_scale(args.spp))
+        log_r(f"[parity] N={world} vs the 1-GPU frame: {parity}")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, crt_amd.camera_floats(cam), log)
+        cpu = cpu_baseline(args, crt.camera_floats(cam), log)
 
     ms_per_step = elapsed / args.steps * 1e3
     value = rays_frame * args.steps / elapsed / 1e6
@@ -598,10 +712,63 @@ def main():
             # N > 1 (or a one-rank process group): each rank's render and the time its stream spent in the collective
             out.update(render_ms_per_rank=dist_t["render_ms_per_rank"], reduce_ms=dist_t["reduce_ms"],
                        reduce_ms_per_rank=dist_t["reduce_ms_per_rank"], dist_timings=dist_t)
+        if world > 1:
+            out["cpu_baseline_note"] = "timed at N=1 only (bench contract): see the N=1 line"
+        if args.share is not None:
+            out["share"] = {"rank": args.share[0], "of": args.share[1], "spp": fr.spp, "subsequence_base": fr.subseq,
+                            "note": "one GPU renders this rank's share of the N-way frame, no collective: value is "
+                                    "the share's rays / s, not a whole-frame figure"}
+        if rehearsal:
+            out["rehearsal"] = (f"--rig {args.rig}: the launch / shard / collective path without the HIP library; "
+                                "measures nothing")
+            out["data"] = "rehearsal: " + out["data"]
         print(json.dumps(out), flush=True)
     if grouped:
+        barrier()    # rank 0's parity frames are local: the others wait here rather than tear the group down early
         dist.destroy_process_group()
+    return 0
+
+
+def statistical_parity(lin_n, rays_n, r, scene, args, world, scale):
+    """N > 1 renders the same estimator with other samples, so its parity with the 1-GPU frame is
+    statistical.  Rank 0 renders the 1-GPU frame F1 (subsequence family 0, all spp) and an independent 1-GPU frame F1'
+    (family N*W*H, disjoint from every rank's); RMS(F1' - F1) = sqrt(2) x the per-image Monte-Carlo noise.  Rank 0's
+    share uses family 0 too, so the N-rank frame shares its first spp/N samples per pixel with F1 and the expected
+    RMS(FN - F1) is sqrt(2) x noise x sqrt(1 - spp_0/spp).  Pass: that ratio within [0.8, 1.25] on every channel and
+    the frame means within 5 standard errors of their difference."""
+    import numpy as np
+    W, H = args.width, args.height
+    frames, rays = [], []
+    for base in (0, world * W * H):
+        r.init_rand(args.seed, base)
+        r.render(scene, args.spp, args.bounces)
+        r.synchronize()
+        frames.append(r.linear().astype(np.float64).reshape(-1, 3) * scale)
+        rays.append(r.counters()["rays"])
+    f1, f1b = frames
+    fn = lin_n.astype(np.float64).reshape(-1, 3) * scale
+    shared = (args.spp // world + (1 if args.spp % world else 0)) / args.spp     # rank 0's share of F1's samples
+    rms_n1 = np.sqrt(np.mean((fn - f1) ** 2, axis=0))
+    rms_11 = np.sqrt(np.mean((f1b - f1) ** 2, axis=0))
+    expected = rms_11 * np.sqrt(1.0 - shared)
+    ratio = rms_n1 / np.maximum(expected, 1e-30)
+    mean_n, mean_1 = fn.mean(axis=0), f1.mean(axis=0)
+    se = rms_n1 / np.sqrt(fn.shape[0])
+    z = np.abs(mean_n - mean_1) / np.maximum(se, 1e-30)
+    ok = bool(np.all((ratio >= 0.8) & (ratio <= 1.25)) and np.all(z <= 5.0))
+    return {"against": f"the 1-GPU frame of the same seed ({args.spp} spp, subsequence family 0)",
+            "kind": "statistical (SURVEY §8e): same estimator, other samples",
+            "frame_mean_per_channel": [round(float(v), 7) for v in mean_n],
+            "frame_mean_1gpu_per_channel": [round(float(v), 7) for v in mean_1],
+            "mean_diff_z": [round(float(v), 3) for v in z],
+            "rms_per_channel": [round(float(v), 7) for v in rms_n1],
+            "rms_two_1gpu_frames_per_channel": [round(float(v), 7) for v in rms_11],
+            "expected_rms_per_channel": [round(float(v), 7) for v in expected],
+            "expected_rule": f"sqrt(2) x MC noise x sqrt(1 - {shared:.4f}) (rank 0's samples are F1's first ones)",
+            "rms_over_expected": [round(float(v), 4) for v in ratio],
+            "rays_rel_diff": (rays_n - rays[0]) / rays[0], "rays_rel_diff_two_1gpu_frames": (rays[1] - rays[0]) / rays[0],
+            "pass": ok, "tolerance": "rms_over_expected in [0.8, 1.25], mean_diff_z <= 5"}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -54,7 +54,7 @@ class ShardedFrameRenderer:
 
     def __init__(self, renderer, scene, spp_total: int, max_bounces: int = 20, seed: int = 41,
                  rank: int = 0, world: int = 1, group=None, reduce_op: str = "reduce", fb_device=None,
-                 mode: str = "spp", collective: bool | None = None):
+                 mode: str = "spp", collective: bool | None = None, local_share: bool = False, max_marks: int = 64):
         if mode not in ("spp", "pixels"):
             raise ValueError("mode must be 'spp' or 'pixels'")
         self.mode = mode
@@ -75,8 +75,11 @@ class ShardedFrameRenderer:
         grp_size = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else None
         if collective is None:
             collective = world > 1 or grp_size == world
-        if world > 1 and not collective:
-            raise ValueError("world > 1 needs the framebuffer collective")
+        if world > 1 and not collective and not local_share:
+            raise ValueError("world > 1 needs the framebuffer collective (local_share=True renders one rank's share "
+                             "alone)")
+        if local_share and (collective or mode != "spp"):
+            raise ValueError("local_share renders one spp share without the collective")
         if collective and grp_size is not None and grp_size != world:
             raise ValueError(f"the process group has {grp_size} ranks but the frame is sharded over world={world}")
         if collective and grp_size is None:
@@ -95,6 +98,7 @@ class ShardedFrameRenderer:
         from . import pixel_sample_scale
         self.scale = pixel_sample_scale(self.spp_total)
         self._marks = []
+        self.max_marks = int(max_marks)
 
     def stream_handle(self):
         if not str(self.fb_device).startswith("cuda"):
@@ -137,7 +141,7 @@ class ShardedFrameRenderer:
                 dist.reduce(self.fb, dst=0, op=dist.ReduceOp.SUM, group=self.group)
         m2 = self._mark()
         self._marks.append((m0, m1, m2))
-        del self._marks[:-64]
+        del self._marks[:-self.max_marks]
         if self.rank == 0 or self.reduce_op == "all_reduce":
             self.r.resolve(self.scale, stream=st)
 
@@ -145,7 +149,8 @@ class ShardedFrameRenderer:
         self._marks = []
 
     def frame_timings(self, last: int | None = None):
-        """[(render_ms, reduce_ms)] of the last `last` frames (all kept frames by default); synchronises first."""
+        """[(render_ms, reduce_ms)] of the last `last` frames (all kept frames, at most max_marks, by default);
+        synchronises first."""
         if str(self.fb_device).startswith("cuda"):
             self.torch.cuda.synchronize(self.r.device)
         marks = self._marks if last is None else self._marks[-last:]
@@ -154,7 +159,8 @@ class ShardedFrameRenderer:
     def linear(self) -> np.ndarray:
         if str(self.fb_device).startswith("cuda"):
             self.torch.cuda.synchronize(self.r.device)
-        return self.fb.cpu().numpy()
+            return self.fb.cpu().numpy()
+        return self.fb.numpy().copy()      # a CPU framebuffer: a copy, not a view later frames overwrite
 
 
 def gather_frame_timings(fr: ShardedFrameRenderer, last: int | None = None, group=None) -> dict:
@@ -166,6 +172,7 @@ def gather_frame_timings(fr: ShardedFrameRenderer, last: int | None = None, grou
     slower ranks; `reduce_ms` is its minimum over ranks (the slowest rank waits least, so its figure is closest to the
     transfer alone), `render_ms_max` the render of the slowest rank."""
     import torch
+    group = fr.group if group is None else group      # the group the frame reduces over
     ft = fr.frame_timings(last)
     n = max(1, len(ft))
     mine = [sum(f[0] for f in ft) / n, sum(f[1] for f in ft) / n]

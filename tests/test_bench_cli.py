@@ -39,6 +39,17 @@ def test_metric_names_the_baseline_config():
     assert bench.workload_name(ns).endswith("(configs[2])")
 
 
+def test_share_counters_fall_back_to_the_whole_frame_per_ray():
+    full = "cornell_bunny_2560x1440_2000spp_20b_rebuilt4"
+    kname = json.loads((REPO / "profiles" / "roofline_counters.json").read_text())[full]["kernel"]
+    e, rule = bench.roofline_counters(full, kname, None)
+    assert e is not None and rule == "own"
+    e2, rule2 = bench.roofline_counters("cornell_bunny_2560x1440_no_such_share", kname, full)
+    assert e2 == e and rule2 == f"per_ray_of:{full}"
+    assert bench.roofline_counters("nope", kname, None) == (None, None)
+    assert bench.roofline_counters(full, "crt_render_kernel<false, 1, 1>", full) == (None, None)
+
+
 def test_roofline_units_from_a_counter_summary():
     e = json.loads((REPO / "profiles" / "roofline_counters.json").read_text())[
         "cornell_bunny_2560x1440_2000spp_20b_rebuilt4"]

@@ -216,6 +216,70 @@ def test_gloo_n2_line_carries_per_rank_timings(scenes):
     assert res[0][1] == res[1][1]   # all_gather: both ranks hold the same table
 
 
+def _subgroup_worker(rank, world, port, files, q):
+    """Ranks 0 and 1 of a 3-rank job shard a frame over a new_group sub-group; gather_frame_timings must run over the
+    frame's own group, so rank 2, outside it, never joins and nothing hangs."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sub = dist.new_group([0, 1])        # every rank must call new_group
+    res = None
+    if rank < 2:
+        import objload
+        import pyoracle
+        from crt_amd.dist import gather_frame_timings
+        o = pyoracle.OracleScene(objload.load_scene(files))
+        r = OracleShardRenderer(o, pyoracle.camera(), W, H)
+        fr = ShardedFrameRenderer(r, None, SPP, 20, 41, rank, 2, group=sub, reduce_op="reduce", fb_device="cpu")
+        fr.render()
+        res = gather_frame_timings(fr)
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_subgroup_frame_timings(scenes):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_subgroup_worker, args=(r, 3, port, scenes["cornell"], q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in ps], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[2][1] is None
+    for _, t in res[:2]:
+        assert t["frames"] == 1 and len(t["render_ms_per_rank"]) == 2
+    assert res[0][1] == res[1][1]
+
+
+def test_mark_history_follows_max_marks():
+    class Null:
+        width, height, device = 4, 2, 0
+
+        def attach_linear(self, p):
+            pass
+
+        def init_rand(self, *a, **k):
+            pass
+
+        def render(self, *a, **k):
+            pass
+
+        def resolve(self, *a, **k):
+            pass
+
+    fr = ShardedFrameRenderer(Null(), None, 4, fb_device="cpu", max_marks=100)
+    for _ in range(90):
+        fr.render()
+    assert len(fr.frame_timings()) == 90
+    with pytest.raises(ValueError):
+        ShardedFrameRenderer(Null(), None, 4, rank=0, world=2, fb_device="cpu", collective=True, local_share=True)
+    share = ShardedFrameRenderer(Null(), None, 5, rank=1, world=2, fb_device="cpu", collective=False, local_share=True)
+    assert (share.spp, share.subseq, share.collective) == (2, 8, False)
+
+
 def test_pixel_mode_argument_checks():
     with pytest.raises(ValueError):
         ShardedFrameRenderer(None, None, 8, mode="rows")

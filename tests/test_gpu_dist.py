@@ -95,6 +95,28 @@ def test_rccl_one_rank_equals_the_unsharded_frame(tmp_path, reduce_op):
     assert int(got["rays"]) == r.counters()["rays"]
 
 
+def test_bench_gpus_2_launches_two_ranks_with_statistical_parity():
+    """bench.py --gpus 2 from a plain `python bench.py` (no launcher environment) starts torch.distributed.run itself;
+    the two ranks share cuda:0 over gloo and render with the HIP kernel.  The line must report n_gpus 2, both ranks'
+    timings and the statistical parity field against the 1-GPU frame."""
+    import json
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    env["OMP_NUM_THREADS"] = "2"
+    p = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--width", "320", "--height", "180", "--spp", "64", "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-4000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["n_gpus"] == 2 and "rehearsal" not in out
+    assert out["config"]["dist_backend"] == "gloo" and out["config"]["kernel_variant"] == 8
+    assert len(out["render_ms_per_rank"]) == 2 and all(v > 0 for v in out["render_ms_per_rank"])
+    par = out["parity"]
+    assert par["kind"].startswith("statistical") and par["pass"] is True, par
+    assert all(0.8 <= v <= 1.25 for v in par["rms_over_expected"])
+    assert abs(par["rays_rel_diff"]) < 0.01
+
+
 def test_three_ranks_uneven_spp(tmp_path):
     """24 spp over 3 ranks (8 each) and the remainder rule; the 3-term fp32 sum order is gloo's, so the check is one
     rounding of the sum, and the frame is the 1-GPU estimator with different samples (statistical, not bitwise)."""
