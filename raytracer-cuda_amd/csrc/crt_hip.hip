@@ -288,12 +288,7 @@ __device__ __forceinline__ int wave_inclusive_scan_shfl(int x, int lane) {
 struct WaveLds {
     float4 ray0[64];                 // o.x, o.y, o.z, d.x of each lane's ray
     float4 ray1[64];                 // d.y, d.z, closest at leaf entry, first prim (int bits)
-#ifdef CRT_LEAF_DUMMY
-    unsigned long long key[128];     // per owner: (t bits << 32) | (0xffffffff - rank), min-reduced; 64..127: per-lane
-                                     // sinks for the rejected pairs' atomics
-#else
     unsigned long long key[64];      // per owner: (t bits << 32) | (0xffffffff - rank), min-reduced
-#endif
     int prefix[64];                  // first pair index of each owner's leaf
     unsigned char owner_at[64];      // owner lane of the pair that starts at each slot of a round
 };
@@ -302,11 +297,7 @@ struct WaveLds {
 struct WaveLdsWide {
     float4 ray0[64];
     float4 ray1[64];
-#ifdef CRT_LEAF_DUMMY
-    unsigned long long key[128];
-#else
     unsigned long long key[64];
-#endif
     unsigned char owner_at[64];
     uint32_t rays;                   // variant 8: the wave's ray count (in LDS, not a VGPR live across the loop)
 #ifdef CRT_CHECKED
@@ -1051,15 +1042,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
             // a rejected pair offers the empty key (no effect on the min): one LDS atomic per pair, no branch
             // (-0.75 %, profiles/r02ar)
             const unsigned long long kp = ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank);
-#ifdef CRT_LEAF_DUMMY
-            atomicMin(&L.key[t >= 0.f ? owner : 64 + lane], kp);
-#elif defined(CRT_LEAF_SELF)
-            // a rejected pair offers the empty key at its own lane's slot (a no-op min on a distinct address), so only
-            // the accepted pairs of one owner contend for the owner's word
-            atomicMin(&L.key[t >= 0.f ? owner : lane], t >= 0.f ? kp : ~0ull);
-#else
             atomicMin(&L.key[owner], t >= 0.f ? kp : ~0ull);
-#endif
         }
         carry = __builtin_amdgcn_readlane(owner1, 63);
         wave_sync();
@@ -1392,10 +1375,6 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     __shared__ float4 shd_lds[WIDE ? 6 : 1];
     __shared__ float4 top_lds[TOPN > 0 ? 8 * TOPN : 1];   // CRT_TOP_LEVELS: root, then its internal children
     __shared__ uint32_t rays0_lds[PERSIST ? 64 * WGW : 1];   // variant 7: the lane's ray count when its pixel started
-#ifdef CRT_LDS_PAD
-    __shared__ float4 pad_lds[CRT_LDS_PAD / 16];          // experiment: LDS footprint alone
-    __asm__ volatile("" : : "v"(&pad_lds[threadIdx.x & 1]));
-#endif
     if (WIDE) {
         if (threadIdx.x < 32) {
             const int k = threadIdx.x & 15;

@@ -193,13 +193,21 @@ struct Run {
     std::vector<int32_t> tri_event;  // per triangle: this run's events before its face
     std::vector<Event> events;
     bool zero_index = false;
+    void swap_into(Run* o) {   // o takes this (empty) run's storage; o's old storage is freed with *this
+        vertices.swap(o->vertices);
+        tri.swap(o->tri);
+        rel.swap(o->rel);
+        tri_event.swap(o->tri_event);
+        events.swap(o->events);
+    }
 };
 
 void parse_run(const char* b, const char* e, Run* R) {
     struct Corner { int32_t v; uint8_t rel; };
     std::vector<Corner> face;
-    // capacity for typical lines ("v x y z" >= 8 bytes a vertex, "f a b c" a triangle), so that the runs' vectors do
-    // not reallocate while other threads parse (an unmapped old block interrupts every thread of the process)
+    // capacity for typical lines ("v x y z" >= 8 bytes a vertex, "f a b c" a triangle): fewer reallocations while
+    // other threads parse (an unmapped old block interrupts every thread of the process).  Denser files (short
+    // integer coordinates, 1-digit indices) still grow the vectors; the capacity is a hint, not a bound
     const size_t bytes = (size_t)(e - b);
     R->vertices.reserve(bytes / 8);
     R->tri.reserve(bytes / 6);
@@ -313,6 +321,7 @@ bool LoadObj(ObjData* out, std::string* err, const char* filename, const char* m
         n_vert += R.vertices.size();
         n_tri += R.tri_event.size();
     }
+    std::string().swap(buf);   // the runs own everything they parsed: the file's bytes go before the outputs come
     out->vertices.resize(n_vert);
     out->triIndices.resize(3 * n_tri);
     out->triMaterial.resize(n_tri);
@@ -323,11 +332,12 @@ bool LoadObj(ObjData* out, std::string* err, const char* filename, const char* m
     }
     parallel_ranges_indexed(runs.size(), [&](size_t, size_t b, size_t e) {
         for (size_t k = b; k < e; ++k) {
-            const Run& R = runs[k];
+            Run& R = runs[k];
             std::copy(R.vertices.begin(), R.vertices.end(), out->vertices.begin() + vb[k]);
             const int32_t vbase = (int32_t)(vb[k] / 3);
             for (size_t i = 0; i < R.tri.size(); ++i) out->triIndices[3 * tb[k] + i] = R.rel[i] ? vbase + R.tri[i] : R.tri[i];
             for (size_t i = 0; i < R.tri_event.size(); ++i) out->triMaterial[tb[k] + i] = mat_after[k][R.tri_event[i]];
+            Run().swap_into(&R);   // each run's memory goes as soon as it is copied, so the peak is ~ the output
         }
     }, 1);
     return true;

