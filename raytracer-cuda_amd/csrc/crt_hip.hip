@@ -1136,7 +1136,20 @@ struct PathState {
     int remaining, bounce;
     bool need_new;
     uint32_t rays, paths;
+#ifdef CRT_PROFILE_LOOPS
+    uint32_t k1, k2, kr;   // this pass: unit-sphere candidates, unit-disk candidates, Russian-roulette draws
+#endif
 };
+#ifdef CRT_PROFILE_LOOPS
+// Profiling build only (tools/build_profile_lib.sh loops -DCRT_PROFILE_LOOPS, tools/loop_fusion_count.py): the
+// regeneration pass's two rejection loops, counted from the XORWOW draw counter (d advances by 362437 per draw;
+// 945708813 is its inverse mod 2^32).  Summed over variant 8's passes: [0] passes, [1] sum of the wave's max unit-sphere
+// candidates, [2] max unit-disk candidates, [3] max over lanes of (sphere + disk candidates), the iteration count of
+// one fused loop, [4] max over lanes of (sphere + RR + disk) draws-steps, [5] lane sum of sphere candidates, [6] lane
+// sum of disk candidates, [7] parked lanes
+__device__ unsigned long long g_loop_prof[8];
+__device__ __forceinline__ uint32_t draws_since(uint32_t d0, uint32_t d1) { return (d1 - d0) * 945708813u; }
+#endif
 
 struct CamRegs {
     V3 pos, llc, hor, ver, right, up;
@@ -1153,12 +1166,18 @@ __device__ __forceinline__ bool next_ray(PathState& S, const CamRegs& C, int x, 
             if (S.remaining == 0) return false;
             --S.remaining;
             float da, db;                                    // Utility::randomPointInUnitDisk
+#ifdef CRT_PROFILE_LOOPS
+            const uint32_t pd0 = S.s.d;
+#endif
             for (;;) {
                 da = rand_pm1(S.s);
                 db = rand_pm1(S.s);
                 if (len2(v3(da, db, 0)) >= 1) continue;
                 break;
             }
+#ifdef CRT_PROFILE_LOOPS
+            S.k2 += draws_since(pd0, S.s.d) / 2u;
+#endif
             const V3 rd = C.lens * v3(da, db, 0);
             const V3 off = v3(C.right.x * rd.x, C.right.y * rd.x, C.right.z * rd.x) +
                            v3(C.up.x * rd.y, C.up.y * rd.y, C.up.z * rd.y);
@@ -1188,6 +1207,9 @@ __device__ __forceinline__ bool next_ray(PathState& S, const CamRegs& C, int x, 
         if (S.bounce >= 3) {
             float p = fmaxf(S.thr.x, fmaxf(S.thr.y, S.thr.z));
             p = fminf(p, 0.95f);
+#ifdef CRT_PROFILE_LOOPS
+            S.kr += 1u;
+#endif
             if (uniform(S.s) > p) {
                 S.pixel = S.pixel + v3(0.0f, 0.0f, 0.0f);
                 ++S.paths;
@@ -1259,7 +1281,13 @@ __device__ __forceinline__ void shade_rec(PathState& S, const RenderParams& P, i
     // Lambertian and Metal both draw one randomUnitVector first (their only draws): one rejection loop for
     // both, so a wave holding both materials does not run the loop twice.
     V3 ruv;
+#ifdef CRT_PROFILE_LOOPS
+    const uint32_t pd0 = S.s.d;
+#endif
     if (code == SHADE_LAMBERT || code == SHADE_METAL) ruv = rand_unit_vector(S.s);
+#ifdef CRT_PROFILE_LOOPS
+    S.k1 += draws_since(pd0, S.s.d) / 3u;
+#endif
     if (code == SHADE_LAMBERT) {                         // Material.cuh:66-77
         V3 sd = n + ruv;
         if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = n;
@@ -1420,6 +1448,10 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     S.pixel = v3(0.f, 0.f, 0.f);
     S.o = v3(0, 0, 0); S.d = v3(0, 0, 1); S.thr = v3(1, 1, 1);
     S.remaining = 0; S.bounce = 0; S.need_new = true; S.rays = 0; S.paths = 0;
+#ifdef CRT_PROFILE_LOOPS
+    S.k1 = S.k2 = S.kr = 0;
+    unsigned long long lp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     if (valid && !PERSIST) {
         const uint32_t* r = P.rng + 6 * (size_t)pix;
         S.s.v0 = r[0]; S.s.v1 = r[1]; S.s.v2 = r[2]; S.s.v3 = r[3]; S.s.v4 = r[4]; S.s.d = r[5];
@@ -1609,6 +1641,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             const bool drain_pass = n_live < regen_t && n_parked * 64 >= n_live * P.wave_drain;
             if (n_parked >= regen_t || n_parked == n_live || drain_pass) {
                 if (COUNT) cnt.passes++;
+#ifdef CRT_PROFILE_LOOPS
+                uint32_t pk1 = 0, pk2 = 0, pkr = 0;
+#endif
                 if (__builtin_amdgcn_inverse_ballot_w64(parked_mask)) {
                     const uint64_t s0 = COUNT ? shader_clock() : 0;
                     // (loading the shading record before this sphere test, to overlap its latency, measured +0.7 %:
@@ -1626,6 +1661,10 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         cnt.cyc_shade += s1 - s0;
                         cnt.cyc_next += s2 - s1;
                     }
+#ifdef CRT_PROFILE_LOOPS
+                    pk1 = S.k1; pk2 = S.k2; pkr = S.kr;
+                    S.k1 = S.k2 = S.kr = 0;
+#endif
                     has_result = false;
                     if (live) {
                         if (!TILED) ++S.rays;
@@ -1645,6 +1684,21 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         if (TOPN > 0) top_steps<COUNT, TOPN>(P, top_lds, S.o, inv, rows, node, sp, cnt, stk, (size_t)pix, n_pix);
                     }
                 }
+#ifdef CRT_PROFILE_LOOPS
+                {
+                    uint32_t m1 = pk1, m2 = pk2, m12 = pk1 + pk2, m1r2 = pk1 + pkr + pk2, s1 = pk1, s2 = pk2;
+                    for (int off = 32; off > 0; off >>= 1) {
+                        m1 = max(m1, (uint32_t)__shfl_xor((int)m1, off));
+                        m2 = max(m2, (uint32_t)__shfl_xor((int)m2, off));
+                        m12 = max(m12, (uint32_t)__shfl_xor((int)m12, off));
+                        m1r2 = max(m1r2, (uint32_t)__shfl_xor((int)m1r2, off));
+                        s1 += (uint32_t)__shfl_xor((int)s1, off);
+                        s2 += (uint32_t)__shfl_xor((int)s2, off);
+                    }
+                    lp[0] += 1; lp[1] += m1; lp[2] += m2; lp[3] += m12; lp[4] += m1r2; lp[5] += s1; lp[6] += s2;
+                    lp[7] += (unsigned long long)n_parked;
+                }
+#endif
                 live_mask = wave_ballot(has_result);
                 first_pass = false;
                 // variant 8 counts the wave's rays in LDS (one VGPR less in the hot loop); (an LDS add without return
@@ -1750,6 +1804,10 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         }
     }
     if (lane == 0) atomicAdd(&P.counters[0], (unsigned long long)wr);
+#ifdef CRT_PROFILE_LOOPS
+    if (lane == 0 && !P.probe_cost)
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_loop_prof[k], lp[k]);
+#endif
 #ifdef CRT_PROFILE_WAVE_TIMES
     {
         const unsigned wid = (blockIdx.y * gridDim.x + blockIdx.x) * (unsigned)WGW + (threadIdx.x >> 6);
@@ -3849,6 +3907,18 @@ extern "C" int crt_profile_live_hist(unsigned long long* out16, int reset) {
     if (reset) {
         static const unsigned long long zero[16] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_live_hist), zero, sizeof zero, 0, hipMemcpyHostToDevice));
+    }
+    return CRT_OK;
+}
+#endif
+#ifdef CRT_PROFILE_LOOPS
+extern "C" int crt_profile_loop_counts(unsigned long long* out8, int reset) {
+    if (!out8) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_loop_prof), 8 * 8, 0, hipMemcpyDeviceToHost));
+    if (reset) {
+        static const unsigned long long zero[8] = {};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_loop_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice));
     }
     return CRT_OK;
 }
