@@ -26,34 +26,47 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
 PKG = REPO / "raytracer-cuda_amd"
-SRC = PKG / "csrc" / "crt_hip.hip"
-DEV = PKG / "csrc" / "crt_device.h"
 
-ap = argparse.ArgumentParser()
-ap.add_argument("--kernel", default="<false, 8, 7>", help="template arguments of crt_render_kernel")
-ap.add_argument("-D", dest="defines", action="append", default=[], help="extra -D flags")
-ap.add_argument("--json", default="", help="also write the tables as JSON here")
-a = ap.parse_args()
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
+         "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize"]
+UNITS = ["VALU", "SALU", "branch", "LDS", "VMEM", "SMEM", "wait/nop", "other"]
 
-m = re.fullmatch(r"<\s*(true|false)\s*,\s*(\d+)\s*,\s*(\d+)\s*>", a.kernel)
-if not m:
-    sys.exit("--kernel must look like '<false, 8, 7>'")
-mangled = f"_Z17crt_render_kernelILb{1 if m.group(1) == 'true' else 0}ELi{m.group(2)}ELi{m.group(3)}EEv12RenderParams"
 
-flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
-         "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize",
-         f"-I{REPO / 'include'}", f"-I{PKG / 'csrc'}", f"-I{PKG / 'host'}"] + [f"-D{d}" for d in a.defines]
-with tempfile.TemporaryDirectory() as td:
-    out = Path(td) / "k.s"
-    p = subprocess.run(["/opt/rocm/bin/hipcc", *flags, "--cuda-device-only", "-gline-tables-only", "-S", "-o", str(out),
-                        str(SRC)], capture_output=True, text=True)
-    if p.returncode:
-        sys.exit(p.stderr[-3000:])
-    asm = out.read_text()
+def mangled_name(kernel: str) -> str:
+    m = re.fullmatch(r"<\s*(true|false)\s*,\s*(\d+)\s*,\s*(\d+)\s*>", kernel)
+    if not m:
+        raise SystemExit("--kernel must look like '<false, 8, 7>'")
+    return f"_Z17crt_render_kernelILb{1 if m.group(1) == 'true' else 0}ELi{m.group(2)}ELi{m.group(3)}EEv12RenderParams"
 
-# file numbers of the .file directives -> source path
-files = {int(n): f for n, f in re.findall(r'^\s*\.file\s+(\d+)\s+"[^"]*"\s+"([^"]+)"', asm, re.M)}
-files.update({int(n): f for n, f in re.findall(r'^\s*\.file\s+(\d+)\s+"([^"]+)"\s*$', asm, re.M)})
+
+def compile_asm(pkg: Path, defines=(), include: Path | None = None):
+    """gfx950 assembly of pkg/csrc/crt_hip.hip with line tables, and the compiler's resource remarks."""
+    flags = FLAGS + [f"-I{include or (pkg.parent / 'include')}", f"-I{pkg / 'csrc'}", f"-I{pkg / 'host'}"] + \
+        [f"-D{d}" for d in defines]
+    with tempfile.TemporaryDirectory() as td:
+        out = Path(td) / "k.s"
+        p = subprocess.run(["/opt/rocm/bin/hipcc", *flags, "--cuda-device-only", "-gline-tables-only", "-S", "-o",
+                            str(out), str(pkg / "csrc" / "crt_hip.hip"), "-Rpass-analysis=kernel-resource-usage"],
+                           capture_output=True, text=True)
+        if p.returncode:
+            raise SystemExit(p.stderr[-3000:])
+        return out.read_text(), p.stderr
+
+
+def resources(remarks: str, mangled: str) -> dict:
+    """The compiler's kernel-resource-usage remark of one kernel: VGPRs, spills, scratch, occupancy, LDS."""
+    out, take = {}, False
+    for line in remarks.splitlines():
+        if "Function Name:" in line:
+            take = mangled in line
+            continue
+        if take and "remark:" in line:
+            k, _, v = line.split("remark:", 1)[1].replace("[-Rpass-analysis=kernel-resource-usage]", "").partition(":")
+            try:
+                out[k.strip()] = int(v.strip())
+            except ValueError:
+                out[k.strip()] = v.strip()
+    return out
 
 
 def heads_of(path: Path):
@@ -66,54 +79,14 @@ def heads_of(path: Path):
     return out
 
 
-HEADS = {"crt_hip.hip": heads_of(SRC), "crt_device.h": heads_of(DEV)}
-SRC_LINES = SRC.read_text().splitlines()
-
-
-def func_of(fname: str, line_no: int) -> str:
-    name = "?"
-    for i, n in HEADS.get(Path(fname).name, []):
-        if i <= line_no:
-            name = n
-        else:
-            break
-    return name
-
-
-def src_line(pattern: str, start_fn: str, after: int = 0) -> int:
-    """The first line after the head of `start_fn` (and after line `after`) containing `pattern` (the line ranges below
-    are anchored on code, not on line numbers)."""
-    start = max(after, next(i for i, n in HEADS["crt_hip.hip"] if n == start_fn))
-    for i in range(start, len(SRC_LINES)):
-        if pattern in SRC_LINES[i - 1]:
-            return i
-    raise SystemExit(f"census anchor not found: {pattern!r} after {start_fn}")
-
-
-# purposes: line ranges inside crt_hip.hip, each [first, last] anchored on a code fragment
-def rng(fn, a_pat, b_pat):
-    lo = src_line(a_pat, fn)
-    return lo, src_line(b_pat, fn, lo)
-
-
-PURPOSES = [
-    ("step: link row / node address", rng("node_step4", "const uint32_t b = node_base(node);", "const int n_int = meta & 0xff;")),
-    ("step: leaf-span sums", rng("node_step4", "uint32_t hm = 0;", "leaf_n = 0;")),
-    ("step: near-first sort", rng("node_step4", "uint32_t k[4];", "cas(k[0], k[1]); cas(k[2], k[3]);")),
-    ("step: push / pop", rng("node_step4", "auto store = [&](int at, uint32_t v) -> bool {", "node = -1;")),
-    ("round: scan + LDS ray record", rng("traverse_step4", "const int incl = wave_inclusive_scan_dpp(leaf_n);",
-                                         "L.key[lane] = ((unsigned long long)ones << 32) | ones;")),
-    ("round: owner lookup", rng("traverse_step4", "if (leaf_n > 0 && pfx >= base && pfx < base + 64)",
-                                "const int j = base + lane;")),
-    ("round: pair record + test + key", rng("traverse_step4", "if (j < total) {", "carry = __builtin_amdgcn_readlane(owner1, 63);")),
-    ("round: per-owner result", rng("traverse_step4", "const unsigned long long kk = L.key[lane];", "hit = rank;")),
-    ("pass: loop head, ballots, drain rule", rng("crt_render_kernel", "const uint64_t parked_mask = live_mask & wave_ballot",
-                                                 "if (__builtin_amdgcn_inverse_ballot_w64(parked_mask)) {")),
-    ("pass: new-ray set-up (1/d, rows, LDS ray)", rng("crt_render_kernel", "if (!TILED) ++S.rays;",
-                                                      "L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);")),
-    ("pass: live mask + ray count", rng("crt_render_kernel", "live_mask = wave_ballot(has_result);",
-                                        "if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);")),
-]
+# sections: the non-helper function (and line range) whose code the instruction belongs to
+SECTION_OF_FUNC = {"node_step4": "node step", "traverse_step4": "leaf rounds", "top_step4": "regeneration pass",
+                   "top_steps": "regeneration pass", "finish_ray": "regeneration pass", "next_ray": "regeneration pass",
+                   "shade_rec": "regeneration pass",
+                   # experiment builds (tools/cost_model.py retro cases): the 8-wide node step (profiles/r05v) and the
+                   # helper-lane step (profiles/r05y)
+                   "node_step8": "node step", "top_step8": "regeneration pass", "node_step4h": "node step",
+                   "traverse_step4h": "leaf rounds"}
 FUNC_PURPOSE = {   # whole helper functions
     "wide_boxes": "box arithmetic (wide_boxes)", "box_inv": "pass: new-ray set-up (1/d, rows, LDS ray)",
     "recip3_exact": "pass: new-ray set-up (1/d, rows, LDS ray)", "ray_rows": "pass: new-ray set-up (1/d, rows, LDS ray)",
@@ -131,20 +104,6 @@ FUNC_PURPOSE = {   # whole helper functions
     "next_ray": "pass: next_ray (RR, camera ray)",
     "top_step4": "pass: LDS root step (top_step4)", "top_steps": "pass: LDS root step (top_step4)",
 }
-DEVICE_H_PURPOSE = "math helpers (crt_device.h)"
-
-# sections: the non-helper function (and line range) whose code the instruction belongs to
-SECTION_OF_FUNC = {"node_step4": "node step", "traverse_step4": "leaf rounds", "top_step4": "regeneration pass",
-                   "top_steps": "regeneration pass", "finish_ray": "regeneration pass", "next_ray": "regeneration pass",
-                   "shade_rec": "regeneration pass"}
-HELPERS = {"wide_boxes", "cas", "ovf_slot", "lane_fresh", "node_base", "node_row", "rec_at", "prim_test",
-           "tri_test_flat", "sphere_candidate", "wave_inclusive_scan_dpp", "wave_inclusive_max_scan_u", "wave_sync",
-           "wave_ballot", "box_inv", "recip3_exact", "ray_rows", "sign_row", "ray_spheres", "ray_spheres2",
-           "sphere_root", "sphere_beyond", "sphere_inv", "ref_scene_box", "cannot_refract_exact", "imax", "better",
-           "shader_clock"}
-KERNEL_PASS = rng("crt_render_kernel", "const uint64_t parked_mask = live_mask & wave_ballot",
-                  "if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);")
-KERNEL_WIDE = rng("crt_render_kernel", "} else if constexpr (WIDE) {", "} else if constexpr (VARIANT == 2 || VARIANT == 3")
 
 
 def unit_of(ins: str) -> str:
@@ -167,82 +126,168 @@ def unit_of(ins: str) -> str:
     return "other"
 
 
-def purpose_of(fname: str, line: int) -> str:
-    if Path(fname).name == "crt_device.h":
-        return f"crt_device.h: {func_of(fname, line)}"
-    if Path(fname).name != "crt_hip.hip":
-        return f"{Path(fname).name}"
-    fn = func_of(fname, line)
-    for name, (lo, hi) in PURPOSES:
-        if lo <= line <= hi:
-            return name
-    if fn in FUNC_PURPOSE:
-        return FUNC_PURPOSE[fn]
-    if fn == "crt_render_kernel":
-        if KERNEL_PASS[0] <= line <= KERNEL_PASS[1]:
-            return "pass: other"
-        if KERNEL_WIDE[0] <= line <= KERNEL_WIDE[1]:
-            return "loop: other"
-        return "kernel prologue / epilogue"
-    return f"{fn}: other"
+def census(pkg: Path = PKG, kernel: str = "<false, 8, 7>", defines=(), purposes: bool = True,
+           include: Path | None = None) -> dict:
+    """Static census of one crt_render_kernel instantiation compiled from pkg/csrc (another revision's tree works as
+    long as its section anchors exist; purposes=False skips the finer purpose anchors).  Returns the unit counts by
+    section and purpose, the VALU by section and purpose, the resource remark and, per section, the VGPR spill
+    accesses (scratch_*) and SGPR-spill read-backs (v_readlane from a spill lane VGPR)."""
+    src_path, dev_path = pkg / "csrc" / "crt_hip.hip", pkg / "csrc" / "crt_device.h"
+    mangled = mangled_name(kernel)
+    asm, remarks = compile_asm(pkg, defines, include)
+    files = {int(n): f for n, f in re.findall(r'^\s*\.file\s+(\d+)\s+"[^"]*"\s+"([^"]+)"', asm, re.M)}
+    files.update({int(n): f for n, f in re.findall(r'^\s*\.file\s+(\d+)\s+"([^"]+)"\s*$', asm, re.M)})
+    heads = {"crt_hip.hip": heads_of(src_path), "crt_device.h": heads_of(dev_path)}
+    src_lines = src_path.read_text().splitlines()
 
+    def func_of(fname: str, line_no: int) -> str:
+        name = "?"
+        for i, n in heads.get(Path(fname).name, []):
+            if i <= line_no:
+                name = n
+            else:
+                break
+        return name
 
-i = asm.index(mangled + ":")
-j = asm.index(".Lfunc_end", i)
-body = asm[i:j].splitlines()
-cur_file, cur_line = "", 0
-owner = "prologue"
-table = defaultdict(Counter)        # purpose -> unit counts
-sections = defaultdict(Counter)     # section -> unit counts
-cross = defaultdict(Counter)        # section -> purpose -> VALU count
-for line in body:
-    t = line.strip()
-    mm = re.match(r"\.loc\s+(\d+)\s+(\d+)", t)
-    if mm:
-        ln = int(mm.group(2))
-        if ln:   # line 0: compiler-made code, keep the last real line
-            cur_file, cur_line = files.get(int(mm.group(1)), ""), ln
-            fn = func_of(cur_file, cur_line) if Path(cur_file).name == "crt_hip.hip" else "crt_device.h"
-            if fn in SECTION_OF_FUNC:
-                owner = SECTION_OF_FUNC[fn]
-            elif fn == "crt_render_kernel":
-                owner = ("regeneration pass" if KERNEL_PASS[0] <= cur_line <= KERNEL_PASS[1]
-                         else "loop head / other" if KERNEL_WIDE[0] <= cur_line <= KERNEL_WIDE[1]
-                         else "prologue / epilogue")
-        continue
-    if not t or t.startswith((".", ";")) or t.endswith(":"):
-        continue
-    u = unit_of(t)
-    pu = purpose_of(cur_file, cur_line)
-    table[pu][u] += 1
-    sections[owner][u] += 1
-    if u == "VALU":
-        cross[owner][pu] += 1
+    def src_line(pattern: str, start_fn: str, after: int = 0) -> int:
+        """The first line after the head of `start_fn` (and after line `after`) containing `pattern` (the line ranges
+        are anchored on code, not on line numbers)."""
+        start = max(after, next(i for i, n in heads["crt_hip.hip"] if n == start_fn))
+        for i in range(start, len(src_lines)):
+            if pattern in src_lines[i - 1]:
+                return i
+        raise SystemExit(f"census anchor not found: {pattern!r} after {start_fn}")
 
-UNITS = ["VALU", "SALU", "branch", "LDS", "VMEM", "SMEM", "wait/nop", "other"]
+    def rng(fn, a_pat, b_pat):
+        lo = src_line(a_pat, fn)
+        return lo, src_line(b_pat, fn, lo)
+
+    purpose_ranges = [
+        ("step: link row / node address", ("node_step4", "const uint32_t b = node_base(node);", "const int n_int = meta & 0xff;")),
+        ("step: leaf-span sums", ("node_step4", "uint32_t hm = 0;", "leaf_n = 0;")),
+        ("step: near-first sort", ("node_step4", "uint32_t k[4];", "cas(k[0], k[1]); cas(k[2], k[3]);")),
+        ("step: push / pop", ("node_step4", "auto store = [&](int at, uint32_t v) -> bool {", "node = -1;")),
+        ("round: scan + LDS ray record", ("traverse_step4", "const int incl = wave_inclusive_scan_dpp(leaf_n);",
+                                          "L.key[lane] = ((unsigned long long)ones << 32) | ones;")),
+        ("round: owner lookup", ("traverse_step4", "if (leaf_n > 0 && pfx >= base && pfx < base + 64)",
+                                 "const int j = base + lane;")),
+        ("round: pair record + test + key", ("traverse_step4", "if (j < total) {", "carry = __builtin_amdgcn_readlane(owner1, 63);")),
+        ("round: per-owner result", ("traverse_step4", "const unsigned long long kk = L.key[lane];", "hit = rank;")),
+        ("pass: loop head, ballots, drain rule", ("crt_render_kernel", "const uint64_t parked_mask = live_mask & wave_ballot",
+                                                  "if (__builtin_amdgcn_inverse_ballot_w64(parked_mask)) {")),
+        ("pass: new-ray set-up (1/d, rows, LDS ray)", ("crt_render_kernel", "if (!TILED) ++S.rays;",
+                                                       "L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);")),
+        ("pass: live mask + ray count", ("crt_render_kernel", "live_mask = wave_ballot(has_result);",
+                                         "first_pass = false;")),
+    ]
+    PURPOSES = [(name, rng(*a)) for name, a in purpose_ranges] if purposes else []
+    kernel_pass = rng("crt_render_kernel", "const uint64_t parked_mask = live_mask & wave_ballot", "first_pass = false;")
+    kernel_wide = rng("crt_render_kernel", "} else if constexpr (WIDE) {", "} else if constexpr (VARIANT == 2 || VARIANT == 3")
+
+    def purpose_of(fname: str, line: int) -> str:
+        if Path(fname).name == "crt_device.h":
+            return f"crt_device.h: {func_of(fname, line)}"
+        if Path(fname).name != "crt_hip.hip":
+            return f"{Path(fname).name}"
+        fn = func_of(fname, line)
+        for name, (lo, hi) in PURPOSES:
+            if lo <= line <= hi:
+                return name
+        if fn in FUNC_PURPOSE:
+            return FUNC_PURPOSE[fn]
+        if fn == "crt_render_kernel":
+            if kernel_pass[0] <= line <= kernel_pass[1]:
+                return "pass: other"
+            if kernel_wide[0] <= line <= kernel_wide[1]:
+                return "loop: other"
+            return "kernel prologue / epilogue"
+        return f"{fn}: other"
+
+    i = asm.index(mangled + ":")
+    j = asm.index(".Lfunc_end", i)
+    body = asm[i:j].splitlines()
+    spill_lanes = {t.strip().split()[1].rstrip(",") for t in body if t.strip().startswith("v_writelane_b32")}
+    cur_file, cur_line = "", 0
+    owner = "prologue"
+    table = defaultdict(Counter)        # purpose -> unit counts
+    sections = defaultdict(Counter)     # section -> unit counts
+    cross = defaultdict(Counter)        # section -> purpose -> VALU count
+    spills = defaultdict(Counter)       # section -> scratch loads / stores, SGPR-spill read-backs
+    for line in body:
+        t = line.strip()
+        mm = re.match(r"\.loc\s+(\d+)\s+(\d+)", t)
+        if mm:
+            ln = int(mm.group(2))
+            if ln:   # line 0: compiler-made code, keep the last real line
+                cur_file, cur_line = files.get(int(mm.group(1)), ""), ln
+                fn = func_of(cur_file, cur_line) if Path(cur_file).name == "crt_hip.hip" else "crt_device.h"
+                if fn in SECTION_OF_FUNC:
+                    owner = SECTION_OF_FUNC[fn]
+                elif fn == "crt_render_kernel":
+                    owner = ("regeneration pass" if kernel_pass[0] <= cur_line <= kernel_pass[1]
+                             else "loop head / other" if kernel_wide[0] <= cur_line <= kernel_wide[1]
+                             else "prologue / epilogue")
+            continue
+        if not t or t.startswith((".", ";")) or t.endswith(":"):
+            continue
+        u = unit_of(t)
+        pu = purpose_of(cur_file, cur_line)
+        table[pu][u] += 1
+        sections[owner][u] += 1
+        if u == "VALU":
+            cross[owner][pu] += 1
+        if t.startswith("scratch_load"):
+            spills[owner]["scratch_load"] += 1
+        elif t.startswith("scratch_store"):
+            spills[owner]["scratch_store"] += 1
+        elif t.startswith("v_readlane_b32"):
+            parts = t.replace(",", " ").split()
+            if len(parts) >= 3 and parts[2] in spill_lanes:
+                spills[owner]["sgpr_readback"] += 1
+    return {"kernel": f"crt_render_kernel{kernel}", "defines": list(defines),
+            "resources": resources(remarks, mangled),
+            "by_section": {k: dict(v) for k, v in sections.items()},
+            "by_purpose": {k: dict(v) for k, v in table.items()},
+            "valu_by_section_purpose": {k: dict(v) for k, v in cross.items()},
+            "spills_by_section": {k: dict(v) for k, v in spills.items()}}
 
 
 def show(title, d):
     print(f"\n{title}")
     print(f"  {'':44s}" + "".join(f"{u:>9s}" for u in UNITS))
     tot = Counter()
-    for k in sorted(d, key=lambda k: -d[k]["VALU"]):
+    for k in sorted(d, key=lambda k: -d[k].get("VALU", 0)):
         tot.update(d[k])
-        print(f"  {k:44s}" + "".join(f"{d[k][u]:9d}" for u in UNITS))
+        print(f"  {k:44s}" + "".join(f"{d[k].get(u, 0):9d}" for u in UNITS))
     print(f"  {'total':44s}" + "".join(f"{tot[u]:9d}" for u in UNITS))
 
 
-print(f"crt_render_kernel{a.kernel}" + (f"  ({' '.join(a.defines)})" if a.defines else "") +
-      ": static instruction census (tools/isa_census.py)")
-show("by section (the section whose code precedes the instruction)", sections)
-show("by purpose (source lines of the instruction)", table)
-print("\nVALU by section and purpose")
-for sec in sorted(cross, key=lambda k: -sum(cross[k].values())):
-    print(f"  {sec} ({sum(cross[sec].values())} VALU)")
-    for pu, n in cross[sec].most_common():
-        print(f"    {n:6d}  {pu}")
-if a.json:
-    Path(a.json).write_text(json.dumps({"kernel": f"crt_render_kernel{a.kernel}", "defines": a.defines,
-                                        "by_section": {k: dict(v) for k, v in sections.items()},
-                                        "by_purpose": {k: dict(v) for k, v in table.items()},
-                                        "valu_by_section_purpose": {k: dict(v) for k, v in cross.items()}}, indent=1))
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", default="<false, 8, 7>", help="template arguments of crt_render_kernel")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra -D flags")
+    ap.add_argument("--json", default="", help="also write the tables as JSON here")
+    a = ap.parse_args()
+    c = census(PKG, a.kernel, a.defines)
+    print(f"crt_render_kernel{a.kernel}" + (f"  ({' '.join(a.defines)})" if a.defines else "") +
+          ": static instruction census (tools/isa_census.py)")
+    res = c["resources"]
+    print("  " + ", ".join(f"{k} {res[k]}" for k in ("VGPRs", "VGPRs Spill", "SGPRs Spill", "ScratchSize [bytes/lane]",
+                                                     "Occupancy [waves/SIMD]") if k in res))
+    show("by section (the section whose code precedes the instruction)", c["by_section"])
+    show("by purpose (source lines of the instruction)", c["by_purpose"])
+    print("\nVALU by section and purpose")
+    cross = c["valu_by_section_purpose"]
+    for sec in sorted(cross, key=lambda k: -sum(cross[k].values())):
+        print(f"  {sec} ({sum(cross[sec].values())} VALU)")
+        for pu, n in sorted(cross[sec].items(), key=lambda kv: -kv[1]):
+            print(f"    {n:6d}  {pu}")
+    print("\nspill accesses by section (scratch loads / stores, SGPR-spill read-backs)")
+    for sec, d in sorted(c["spills_by_section"].items()):
+        print(f"  {sec:28s} " + ", ".join(f"{k} {v}" for k, v in sorted(d.items())))
+    if a.json:
+        Path(a.json).write_text(json.dumps(c, indent=1))
+
+
+if __name__ == "__main__":
+    main()
