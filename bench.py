@@ -127,9 +127,6 @@ def parse(argv=None):
                     help="variants 4/8: a draining wave passes at this many 64ths of its live lanes (64 = all)")
     ap.add_argument("--drain-threshold", type=int, default=None,
                     help="variant 7: regeneration threshold once the pixel queue is empty (0 = unchanged)")
-    ap.add_argument("--sphere-cap", type=int, default=None,
-                    help="variants 4/8: unit-sphere candidates per pass before a lane defers (crt_renderer_set_sphere_cap; "
-                         "0 = no cap; default: the library's)")
     ap.add_argument("--xcd-regions", type=int, default=None, choices=[0, 1],
                     help="variant 8: XCD groups render equal-cost screen strips (crt_renderer_set_xcd_regions)")
     ap.add_argument("--bvh", default="rebuilt", choices=["rebuilt", "reference"])
@@ -497,8 +494,6 @@ def run(args) -> int:
             rr.set_critical_tiles(args.critical_tiles, args.critical_lanes)
         if args.xcd_regions is not None:
             rr.set_xcd_regions(args.xcd_regions)
-        if args.sphere_cap is not None:
-            rr.set_sphere_cap(args.sphere_cap)
         if args.drain_threshold is not None:
             rr.set_drain_threshold(args.drain_threshold)
         if args.wave_drain is not None:

@@ -285,12 +285,6 @@ int  crt_renderer_set_drain_threshold(crt_renderer* r, int lanes);
  * runs when `sixty_fourths`/64 of those live lanes are parked (1..64; 64 = only when all of them are; default 48), so
  * the wave's last pixels wait less for each other's paths.  Results never depend on it. */
 int  crt_renderer_set_wave_drain(crt_renderer* r, int sixty_fourths);
-/* Variants 4 and 8: a lane's unit-sphere rejection loop (Lambertian / metal scatter, Utility.cuh:45-53) draws at most
- * `candidates` candidates per shading pass (0 = no cap, 1..64); a lane that has not accepted one by then keeps its hit
- * parked and goes on with the same candidate sequence at the wave's next pass, so the wave no longer waits for its
- * unluckiest lane's draws in every pass.  Every lane draws the same candidates in the same order: results never depend
- * on it. */
-int  crt_renderer_set_sphere_cap(crt_renderer* r, int candidates);
 /* Variant 8 with the cost probe: 1 = the blocks that share an XCD (block index mod 8, MI355X's round-robin dispatch)
  * render one screen strip of equal probe cost, most expensive tile first, so each XCD's L2 holds its strip's geometry;
  * 0 = one global cost order (default).  Ignored with pixel sharding.  Results never depend on it. */

@@ -322,11 +322,6 @@ class Renderer:
         """Variants 4/8: a draining wave passes at sixty_fourths/64 of its live lanes (crt_renderer_set_wave_drain)."""
         check(_lib.hip().crt_renderer_set_wave_drain(self.h, int(sixty_fourths)), "set_wave_drain")
 
-    def set_sphere_cap(self, candidates: int):
-        """Variants 4/8: unit-sphere candidates a lane draws per pass before it defers to the next (0 = no cap;
-        crt_renderer_set_sphere_cap).  Results never depend on it."""
-        check(_lib.hip().crt_renderer_set_sphere_cap(self.h, int(candidates)), "set_sphere_cap")
-
     def set_xcd_regions(self, on: bool):
         """Variant 8: XCD groups render equal-cost screen strips (crt_renderer_set_xcd_regions)."""
         check(_lib.hip().crt_renderer_set_xcd_regions(self.h, int(bool(on))), "set_xcd_regions")

@@ -105,7 +105,7 @@ HIP_SYMBOLS = [
     "crt_renderer_rgba_device_ptr", "crt_renderer_rng_device_ptr", "crt_renderer_last_kernel_ms",
     "crt_renderer_last_kernel_name", "crt_renderer_last_timings", "crt_renderer_timing_history",
     "crt_renderer_set_leaf_carry", "crt_renderer_set_xcd_regions", "crt_renderer_set_temporal_order",
-    "crt_renderer_set_drain_threshold", "crt_renderer_set_wave_drain", "crt_renderer_set_sphere_cap",
+    "crt_renderer_set_drain_threshold", "crt_renderer_set_wave_drain",
     "crt_renderer_attach_linear", "crt_renderer_set_kernel_variant", "crt_renderer_get_schedule_stats",
     "crt_renderer_set_regen_threshold", "crt_renderer_set_occupancy_target",
     "crt_build_mesh_bvh", "crt_renderer_set_schedule", "crt_renderer_set_critical_tiles", "crt_renderer_set_pixel_shard",
@@ -170,7 +170,6 @@ def hip():
             "crt_renderer_set_temporal_order": ([P, i32], i32),
             "crt_renderer_set_drain_threshold": ([P, i32], i32),
             "crt_renderer_set_wave_drain": ([P, i32], i32),
-            "crt_renderer_set_sphere_cap": ([P, i32], i32),
             "crt_renderer_read_linear": ([P, P], i32), "crt_renderer_read_rgba8": ([P, P], i32),
             "crt_renderer_read_rng": ([P, P], i32), "crt_renderer_write_linear": ([P, P], i32),
             "crt_renderer_get_counters": ([P, P], i32),

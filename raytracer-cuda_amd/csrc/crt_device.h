@@ -163,23 +163,6 @@ __device__ __forceinline__ V3 rand_unit_vector(Rng& s) {   // Utility.cuh:45-53,
     }
     return unit(p);
 }
-// The same loop stopped after `cap` rejected candidates (false: no candidate accepted, the draws made stay made); a
-// later call continues the same sequence of candidates from the advanced state.
-__device__ __forceinline__ bool rand_unit_vector_capped(Rng& s, int cap, V3& out) {
-    V3 p;
-    bool ok = false;
-    for (int k = 0; k < cap; ++k) {
-        float a = rand_pm1(s);
-        float b = rand_pm1(s);
-        float c = rand_pm1(s);
-        p = v3(a, b, c);
-        if (len2(p) >= 1) continue;
-        ok = true;
-        break;
-    }
-    if (ok) out = unit(p);
-    return ok;
-}
 
 // Material.cuh:132-137 with pow(float,int) restated as exponentiation by squaring.  r0 = ((1 - ref_idx) /
 // (1 + ref_idx))^2 depends on the material and the face only: the shading record carries it (schlick_r0 in

@@ -88,7 +88,6 @@ struct RenderParams {
     int drain_threshold;                  // variant 7: the threshold once the pixel queue is empty
     int wave_drain;                       // variants 4/8: sixty-fourths of the live lanes a draining wave passes at
     int top_levels;                       // 4-wide variants: a new ray's first node steps taken from LDS (<= CRT_TOP_LEVELS)
-    int sphere_cap;                       // variants 4/8: unit-sphere candidates per pass before a lane defers (0 = none)
 };
 
 #ifdef CRT_PROFILE_LIVE
@@ -1246,8 +1245,8 @@ __device__ __forceinline__ bool cannot_refract_exact(float cos_theta, float ri) 
 // material come from its shading record (crt_device.h): one pair of independent loads per hit.
 // shade_rec: the same with the hit's shading record rows 0-1 already loaded (r0, m); a sphere's row 2 (1 / radius) is
 // inv_r when `staged`, else loaded here.
-__device__ __forceinline__ bool shade_rec(PathState& S, const RenderParams& P, int hit_rank, float t, float4 r0,
-                                          float4 m, bool staged, float inv_r, int cap = 0);
+__device__ __forceinline__ void shade_rec(PathState& S, const RenderParams& P, int hit_rank, float t, float4 r0,
+                                          float4 m, bool staged, float inv_r);
 __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int hit_rank, float t) {
     float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), m = r0;
     if (hit_rank >= 0) {
@@ -1255,15 +1254,15 @@ __device__ __forceinline__ void shade(PathState& S, const RenderParams& P, int h
         r0 = R[0];
         m = R[1];
     }
-    (void)shade_rec(S, P, hit_rank, t, r0, m, false, 0.f);
+    shade_rec(S, P, hit_rank, t, r0, m, false, 0.f);
 }
-__device__ __forceinline__ bool shade_rec(PathState& S, const RenderParams& P, int hit_rank, float t, float4 r0,
-                                          float4 m, bool staged, float inv_r, int cap) {
+__device__ __forceinline__ void shade_rec(PathState& S, const RenderParams& P, int hit_rank, float t, float4 r0,
+                                          float4 m, bool staged, float inv_r) {
     if (hit_rank < 0) {                                  // :137-142
         S.pixel = S.pixel + S.thr * sky(S.d);
         ++S.paths;
         S.need_new = true;
-        return true;
+        return;
     }
     const uint32_t kind = __float_as_uint(r0.w);
     const V3 hp = S.o + t * S.d;                         // Ray::pointAtDistance
@@ -1277,7 +1276,7 @@ __device__ __forceinline__ bool shade_rec(PathState& S, const RenderParams& P, i
     const uint32_t code = kind & 15u;
     if (code == SHADE_INVALID) {                         // :127 invalid material: same ray again
         ++S.bounce;
-        return true;
+        return;
     }
     // Lambertian and Metal both draw one randomUnitVector first (their only draws): one rejection loop for
     // both, so a wave holding both materials does not run the loop twice.
@@ -1285,17 +1284,7 @@ __device__ __forceinline__ bool shade_rec(PathState& S, const RenderParams& P, i
 #ifdef CRT_PROFILE_LOOPS
     const uint32_t pd0 = S.s.d;
 #endif
-    // cap > 0 (variant 8's pass, RenderParams::sphere_cap): after `cap` rejected candidates the lane stops here with
-    // nothing of the path changed but the draws it made, and the caller keeps it parked with its hit; the next pass
-    // runs finish_ray again and the loop goes on from the same RNG state, so every lane draws the same candidates in
-    // the same order as without the cap ("capped unit-sphere loop")
-    if (code == SHADE_LAMBERT || code == SHADE_METAL) {
-        if (cap > 0) {
-            if (!rand_unit_vector_capped(S.s, cap, ruv)) return false;
-        } else {
-            ruv = rand_unit_vector(S.s);
-        }
-    }
+    if (code == SHADE_LAMBERT || code == SHADE_METAL) ruv = rand_unit_vector(S.s);
 #ifdef CRT_PROFILE_LOOPS
     S.k1 += draws_since(pd0, S.s.d) / 3u;
 #endif
@@ -1339,7 +1328,6 @@ __device__ __forceinline__ bool shade_rec(PathState& S, const RenderParams& P, i
         ++S.paths;
         S.need_new = true;
     }
-    return true;
 }
 
 // A parked lane's end of trace in the regeneration pass (4-wide variants): the per-ray spheres (Sphere::hit behind the
@@ -1347,9 +1335,8 @@ __device__ __forceinline__ bool shade_rec(PathState& S, const RenderParams& P, i
 // behind a compiler barrier, so its latency hides behind that test (-0.6 %, profiles/r03aa); when a per-ray sphere
 // wins, its record comes from the LDS copy of the two per-ray spheres' records (or from HBM for other sphere counts).
 template <bool COUNT>
-__device__ __forceinline__ bool finish_ray(PathState& S, const RenderParams& P, V3 inv, float closest, int hit,
-                                           const float* sph_lds, const float4* shd_lds, TraceCounts& cnt, uint64_t s0,
-                                           int cap = 0) {
+__device__ __forceinline__ void finish_ray(PathState& S, const RenderParams& P, V3 inv, float closest, int hit,
+                                           const float* sph_lds, const float4* shd_lds, TraceCounts& cnt, uint64_t s0) {
     const int h0 = hit;
     float4 e0 = make_float4(0.f, 0.f, 0.f, 0.f), e1 = e0;
     if (h0 >= 0) {
@@ -1376,7 +1363,7 @@ __device__ __forceinline__ bool finish_ray(PathState& S, const RenderParams& P, 
             e1 = Rh[1];
         }
     }
-    return shade_rec(S, P, hit, closest, e0, e1, staged, inv_r, cap);
+    shade_rec(S, P, hit, closest, e0, e1, staged, inv_r);
 }
 
 // VARIANT 0: per-lane traversal (leaf loops inside the lane).  VARIANT 1: cooperative leaves.
@@ -1657,7 +1644,6 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
 #ifdef CRT_PROFILE_LOOPS
                 uint32_t pk1 = 0, pk2 = 0, pkr = 0;
 #endif
-                bool started = false;    // a new ray this pass (a deferred lane keeps its parked hit)
                 if (__builtin_amdgcn_inverse_ballot_w64(parked_mask)) {
                     const uint64_t s0 = COUNT ? shader_clock() : 0;
                     // (loading the shading record before this sphere test, to overlap its latency, measured +0.7 %:
@@ -1665,12 +1651,11 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     // after the first pass every parked lane holds a result (parked_mask is within live_mask, which is
                     // the lanes with a ray): a uniform test instead of a divergent branch on has_result (-0.38 %,
                     // profiles/r02av)
-                    bool deferred = false;   // the lane's capped unit-sphere loop goes on at the next pass
                     if (!first_pass) {
-                        deferred = !finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, s0, P.sphere_cap);
+                        finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, s0);
                     }
                     const uint64_t s1 = COUNT ? shader_clock() : 0;
-                    const bool live = deferred || next_ray(S, C, x, y, P.max_bounces);
+                    const bool live = next_ray(S, C, x, y, P.max_bounces);
                     if (COUNT) {
                         const uint64_t s2 = shader_clock();
                         cnt.cyc_shade += s1 - s0;
@@ -1680,10 +1665,10 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     pk1 = S.k1; pk2 = S.k2; pkr = S.kr;
                     S.k1 = S.k2 = S.kr = 0;
 #endif
-                    has_result = live;
-                    started = live && !deferred;
-                    if (started) {
+                    has_result = false;
+                    if (live) {
                         if (!TILED) ++S.rays;
+                        has_result = true;
                         node = 0;
                         sp = 0;
                         closest = INF;
@@ -1718,10 +1703,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 first_pass = false;
                 // variant 8 counts the wave's rays in LDS (one VGPR less in the hot loop); (an LDS add without return
                 // instead of the read-modify-write measured +0.4 % on config C, profiles/r05e)
-                if (TILED) {
-                    const uint64_t started_mask = wave_ballot(started);
-                    if (lane == 0) L.rays += (uint32_t)__popcll(started_mask);
-                }
+                if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);
             }
             if (COUNT) cnt.cyc_regen += shader_clock() - c0;
             traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
@@ -2904,7 +2886,6 @@ struct crt_renderer {
     int temporal = 0;              // variant 7: tiles ordered by the previous variant-7 frame's rays per pixel
     int drain_threshold = 0;       // variant 7: regeneration threshold once the pixel queue is empty (0 = unchanged)
     int wave_drain = 48;           // variants 4/8: draining waves pass at 48/64 of their live lanes (profiles/r04n)
-    int sphere_cap = 0;            // variants 4/8: unit-sphere candidates per pass before a lane defers (0 = no cap)
     uint32_t* d_pix_rays = nullptr;   // variant 7 with the temporal order: rays per pixel of the last frame
     uint32_t* d_tile_order = nullptr; // its tiles, most expensive first
     bool pix_rays_valid = false;
@@ -3445,7 +3426,6 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     P.regen_threshold = S->width == 4 ? R->regen_threshold_wide : R->regen_threshold;
     P.drain_threshold = R->drain_threshold > 0 ? R->drain_threshold : P.regen_threshold;
     P.wave_drain = R->wave_drain;
-    P.sphere_cap = S->width == 4 ? R->sphere_cap : 0;
     if (R->tile_shards > 1) {
         // pixel sharding: variant 8 renders this shard's tiles; every other pixel of the framebuffer is 0, so the sum
         // of the shards' framebuffers (one collective) is the unsharded frame exactly (x + 0 = x).  Checked and
@@ -3981,12 +3961,6 @@ int crt_renderer_set_drain_threshold(crt_renderer* R, int lanes) {
 int crt_renderer_set_wave_drain(crt_renderer* R, int sixty_fourths) {
     if (!R || sixty_fourths < 1 || sixty_fourths > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "wave drain 1..64");
     R->wave_drain = sixty_fourths;
-    return CRT_OK;
-}
-
-int crt_renderer_set_sphere_cap(crt_renderer* R, int candidates) {
-    if (!R || candidates < 0 || candidates > 64) return set_error(CRT_ERR_INVALID_ARGUMENT, "sphere cap 0..64");
-    R->sphere_cap = candidates;
     return CRT_OK;
 }
 
