@@ -105,8 +105,20 @@ struct TraceCounts {
     uint64_t cyc_regen, cyc_step, cyc_round, passes;
     uint64_t cyc_shade, cyc_next;   // inside the regen pass: ray_spheres() + shade(), next_ray(); the rest is ray init
     uint64_t cyc_sph;               // of cyc_shade: the per-ray spheres (ray_spheres)
+    uint64_t cyc_setup, cyc_top, cyc_head;   // CRT_PROFILE_PASS: new-ray set-up, LDS root step, loop head
 };
 __device__ __forceinline__ uint64_t shader_clock() { return __builtin_amdgcn_s_memtime(); }
+// Profiling build only (tools/build_profile_lib.sh pass -DCRT_PROFILE_PASS, tools/pass_profile.py): the section timers
+// the counting kernel keeps (s_memtime per section) also in the timed kernel, with the regeneration pass split into
+// its parts.  g_pass_prof, summed over variant 8's waves: [0] step, [1] rounds, [2] pass total, [3] finish_ray (spheres
+// + shade), [4] of which the per-ray spheres, [5] next_ray, [6] new-ray set-up (1/d, rows, LDS ray record), [7] the
+// LDS root step (top_steps), [8] loop head (live / parked ballots, the drain rule), [9] passes, [10] waves
+#ifdef CRT_PROFILE_PASS
+constexpr bool kProfilePass = true;
+__device__ unsigned long long g_pass_prof[12];
+#else
+constexpr bool kProfilePass = false;
+#endif
 
 // Hit rule shared by every variant and both BVH modes: a candidate (t, rank) replaces the current hit
 // when t < closest, or t == closest and its reference DFS rank is higher.  In CRT_BVH_REFERENCE mode the
@@ -975,12 +987,13 @@ template <bool COUNT>
 __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
                                                float& closest, int& hit, TraceCounts& cnt, WaveLdsWide& L,
                                                uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix) {
+    constexpr bool TIME = COUNT || kProfilePass;
     if (COUNT) cnt.step_slots++;
-    const uint64_t c0 = COUNT ? shader_clock() : 0;
+    const uint64_t c0 = TIME ? shader_clock() : 0;
     int leaf_n, leaf_first;
     node_step4<COUNT>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
-    const uint64_t c1 = COUNT ? shader_clock() : 0;
-    if (COUNT) cnt.cyc_step += c1 - c0;
+    const uint64_t c1 = TIME ? shader_clock() : 0;
+    if (TIME) cnt.cyc_step += c1 - c0;
 #ifdef CRT_PROFILE_PAIRS
     // profiling build (tools/pair_histogram.py): per wave step, the lanes stepping and the leaf pairs, log2 buckets
     {
@@ -1056,7 +1069,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
             hit = rank;
         }
     }
-    if (COUNT) cnt.cyc_round += shader_clock() - c1;
+    if (TIME) cnt.cyc_round += shader_clock() - c1;
 }
 
 // The tree's top nodes held in LDS (CRT_TOP_LEVELS): the root and, at level 2, its internal children, copied once
@@ -1347,7 +1360,7 @@ __device__ __forceinline__ void finish_ray(PathState& S, const RenderParams& P, 
     __asm__ volatile("" : : : "memory");   // keep the loads ahead of the sphere test
     ray_spheres<true>(P.prims, P.sphere_chain, P.n_chain, P.sphere_first, P.n_ray_spheres, S.o, S.d,
                       sphere_inv(S.d, inv), closest, hit, sph_lds);
-    if (COUNT) cnt.cyc_sph += shader_clock() - s0;
+    if (COUNT || kProfilePass) cnt.cyc_sph += shader_clock() - s0;
     bool staged = false;
     float inv_r = 0.f;
     if (hit != h0 && hit >= 0) {   // a per-ray sphere won: its record from LDS (two spheres) or HBM
@@ -1472,7 +1485,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     C.rfw = P.rcp_w;
     C.rfh = P.rcp_h;
     C.fast_uv = P.fast_uv;
-    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t wave_rays = 0;    // variant 8: rays of the wave (uniform); the other variants count per lane
 
     if constexpr (VARIANT == 0) {
@@ -1614,7 +1627,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         uint64_t lt_prev = shader_clock();
         int lb_prev = 8;
 #endif
+        constexpr bool TIME = COUNT || kProfilePass;
         for (;;) {
+            const uint64_t h0 = kProfilePass ? shader_clock() : 0;
             const uint64_t parked_mask = live_mask & wave_ballot(node < 0);
             const int n_parked = __popcll(parked_mask);
             const int n_live = __popcll(live_mask);
@@ -1634,18 +1649,19 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
             }
 #endif
             if (n_live == 0) break;
-            const uint64_t c0 = COUNT ? shader_clock() : 0;
+            const uint64_t c0 = TIME ? shader_clock() : 0;
+            if (kProfilePass) cnt.cyc_head += c0 - h0;
             // once fewer than regen_t lanes still have samples, waiting for every live lane to park before a pass makes
             // each of them wait for the slowest path of the others at every bounce; a pass at wave_drain/64 of them
             // (crt_renderer_set_wave_drain; 64 = all) shortens the wave's own drain (profiles/r04n)
             const bool drain_pass = n_live < regen_t && n_parked * 64 >= n_live * P.wave_drain;
             if (n_parked >= regen_t || n_parked == n_live || drain_pass) {
-                if (COUNT) cnt.passes++;
+                if (COUNT || kProfilePass) cnt.passes++;
 #ifdef CRT_PROFILE_LOOPS
                 uint32_t pk1 = 0, pk2 = 0, pkr = 0;
 #endif
                 if (__builtin_amdgcn_inverse_ballot_w64(parked_mask)) {
-                    const uint64_t s0 = COUNT ? shader_clock() : 0;
+                    const uint64_t s0 = TIME ? shader_clock() : 0;
                     // (loading the shading record before this sphere test, to overlap its latency, measured +0.7 %:
                     // profiles/r01ar)
                     // after the first pass every parked lane holds a result (parked_mask is within live_mask, which is
@@ -1654,9 +1670,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     if (!first_pass) {
                         finish_ray<COUNT>(S, P, inv, closest, hit, sph_lds, shd_lds, cnt, s0);
                     }
-                    const uint64_t s1 = COUNT ? shader_clock() : 0;
+                    const uint64_t s1 = TIME ? shader_clock() : 0;
                     const bool live = next_ray(S, C, x, y, P.max_bounces);
-                    if (COUNT) {
+                    if (TIME) {
                         const uint64_t s2 = shader_clock();
                         cnt.cyc_shade += s1 - s0;
                         cnt.cyc_next += s2 - s1;
@@ -1681,7 +1697,13 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                         if (COUNT) cnt.spheres += P.n_ray_spheres;
                         L.ray0[lane] = make_float4(S.o.x, S.o.y, S.o.z, S.d.x);
                         if (COUNT) cnt.trace_calls++;
+                        const uint64_t s3 = kProfilePass ? shader_clock() : 0;
                         if (TOPN > 0) top_steps<COUNT, TOPN>(P, top_lds, S.o, inv, rows, node, sp, cnt, stk, (size_t)pix, n_pix);
+                        if (kProfilePass) {
+                            const uint64_t s4 = shader_clock();
+                            cnt.cyc_top += s4 - s3;
+                            cnt.cyc_setup += s3 - s1;   // next_ray and the set-up; next_ray's share is subtracted below
+                        }
                     }
                 }
 #ifdef CRT_PROFILE_LOOPS
@@ -1703,9 +1725,13 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 first_pass = false;
                 // variant 8 counts the wave's rays in LDS (one VGPR less in the hot loop); (an LDS add without return
                 // instead of the read-modify-write measured +0.4 % on config C, profiles/r05e)
+#ifdef CRT_RAYS_SGPR
+                if (TILED) wave_rays += (uint32_t)__popcll(parked_mask & live_mask);
+#else
                 if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);
+#endif
             }
-            if (COUNT) cnt.cyc_regen += shader_clock() - c0;
+            if (TIME) cnt.cyc_regen += shader_clock() - c0;
             traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
         }
     } else if constexpr (VARIANT == 2 || VARIANT == 3 || VARIANT == 10) {
@@ -1779,7 +1805,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         P.sum[3 * (size_t)pix + 1] = S.pixel.y;
         P.sum[3 * (size_t)pix + 2] = S.pixel.z;
     }
+#ifndef CRT_RAYS_SGPR
     if constexpr (TILED) wave_rays = lds[0].rays;
+#endif
     const uint64_t wr = TILED ? (uint64_t)wave_rays : wave_sum_u64(S.rays);
     if (COUNT) {
         const uint64_t wb = wave_sum_u64(cnt.boxes), wt = wave_sum_u64(cnt.tris);
@@ -1804,6 +1832,13 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         }
     }
     if (lane == 0) atomicAdd(&P.counters[0], (unsigned long long)wr);
+#ifdef CRT_PROFILE_PASS
+    if (!COUNT && TILED && lane == 0) {
+        const unsigned long long v[11] = {cnt.cyc_step, cnt.cyc_round, cnt.cyc_regen, cnt.cyc_shade, cnt.cyc_sph,
+                                          cnt.cyc_next, cnt.cyc_setup, cnt.cyc_top, cnt.cyc_head, cnt.passes, 1ull};
+        for (int k = 0; k < 11; ++k) atomicAdd(&g_pass_prof[k], v[k]);
+    }
+#endif
 #ifdef CRT_PROFILE_LOOPS
     if (lane == 0 && !P.probe_cost)
         for (int k = 0; k < 8; ++k) atomicAdd(&g_loop_prof[k], lp[k]);
@@ -1860,7 +1895,7 @@ __global__ __launch_bounds__(256) void crt_compare_kernel(CompareParams Q) {
     C.rfw = P.rcp_w;
     C.rfh = P.rcp_h;
     C.fast_uv = P.fast_uv;
-    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    TraceCounts cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long n_rank = 0, n_t = 0, n_bmiss = 0, n_amiss = 0;
     while (next_ray(S, C, x, y, P.max_bounces)) {
         ++S.rays;
@@ -3907,6 +3942,18 @@ extern "C" int crt_profile_live_hist(unsigned long long* out16, int reset) {
     if (reset) {
         static const unsigned long long zero[16] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_live_hist), zero, sizeof zero, 0, hipMemcpyHostToDevice));
+    }
+    return CRT_OK;
+}
+#endif
+#ifdef CRT_PROFILE_PASS
+extern "C" int crt_profile_pass_sections(unsigned long long* out12, int reset) {
+    if (!out12) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_pass_prof), 12 * 8, 0, hipMemcpyDeviceToHost));
+    if (reset) {
+        static const unsigned long long zero[12] = {};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pass_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice));
     }
     return CRT_OK;
 }
