@@ -1725,11 +1725,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 first_pass = false;
                 // variant 8 counts the wave's rays in LDS (one VGPR less in the hot loop); (an LDS add without return
                 // instead of the read-modify-write measured +0.4 % on config C, profiles/r05e)
-#ifdef CRT_RAYS_SGPR
-                if (TILED) wave_rays += (uint32_t)__popcll(parked_mask & live_mask);
-#else
                 if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);
-#endif
             }
             if (TIME) cnt.cyc_regen += shader_clock() - c0;
             traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
@@ -1805,9 +1801,7 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         P.sum[3 * (size_t)pix + 1] = S.pixel.y;
         P.sum[3 * (size_t)pix + 2] = S.pixel.z;
     }
-#ifndef CRT_RAYS_SGPR
     if constexpr (TILED) wave_rays = lds[0].rays;
-#endif
     const uint64_t wr = TILED ? (uint64_t)wave_rays : wave_sum_u64(S.rays);
     if (COUNT) {
         const uint64_t wb = wave_sum_u64(cnt.boxes), wt = wave_sum_u64(cnt.tris);
