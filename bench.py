@@ -731,32 +731,45 @@ def run(args) -> int:
 
 def statistical_parity(lin_n, rays_n, r, scene, args, world, scale):
     """N > 1 renders the same estimator with other samples, so its parity with the 1-GPU frame is
-    statistical.  Rank 0 renders the 1-GPU frame F1 (subsequence family 0, all spp) and an independent 1-GPU frame F1'
-    (family N*W*H, disjoint from every rank's); RMS(F1' - F1) = sqrt(2) x the per-image Monte-Carlo noise.  Rank 0's
-    share uses family 0 too, so the N-rank frame shares its first spp/N samples per pixel with F1 and the expected
-    RMS(FN - F1) is sqrt(2) x noise x sqrt(1 - spp_0/spp).  The frame means are compared on the displayed values
-    (writeColor's gamma and clamp, Color.cuh): the linear sums carry the glass caustics' rare, very bright paths, whose
-    heavy tail makes a linear mean test unreliable at a few standard errors (it is reported too, with the same test on
-    the two independent 1-GPU frames as a control).  Pass: the RMS ratio within [0.8, 1.25] on every channel and the
-    displayed means within 5 standard errors of their difference."""
+    statistical.  Rank 0 renders the 1-GPU frame F1 (subsequence family 0, all spp), an independent 1-GPU frame F1'
+    (family 2N·W·H) and an independent N-way frame F_N' (the N shares from families N .. 2N-1, summed).
+
+    * Per pixel: RMS(F1' - F1) = sqrt(2) x the Monte-Carlo noise; rank 0's share uses family 0 too, so the N-rank frame
+      shares its first spp/N samples per pixel with F1 and the expected RMS(F_N - F1) is sqrt(2) x noise x
+      sqrt(1 - spp_0/spp).  Pass: the measured / expected ratio within [0.8, 1.25] on every channel.
+    * Frame mean: F_N against F_N', the exchangeable frame (the same number of streams and samples per stream), on the
+      displayed values (writeColor's gamma and clamp).  Pass: within 5 standard errors of their difference.  The mean
+      against F1 is reported too: at 3.7 M pixels a frame of 2000 consecutive samples per pixel stream and a sum of N
+      shorter streams differ by a few 1e-4 of the mean, in a seed-dependent direction, beyond the independent-pixel
+      noise model (profiles/r06k: F_N vs F_N' and F1 vs F1' agree, single- vs multi-stream frames do not), so the 1-GPU
+      frame is not an exchangeable control for the mean."""
     import numpy as np
     W, H = args.width, args.height
-    frames, rays = [], []
-    for base in (0, world * W * H):
+    rays = []
+
+    def frame(base, spp):
         r.init_rand(args.seed, base)
-        r.render(scene, args.spp, args.bounces)
+        r.render(scene, spp, args.bounces)
         r.synchronize()
-        frames.append(r.linear().astype(np.float64).reshape(-1, 3) * scale)
         rays.append(r.counters()["rays"])
-    f1, f1b = frames
+        return r.linear().astype(np.float64).reshape(-1, 3)
+
+    def share_spp(g):
+        return args.spp // world + (1 if g < args.spp % world else 0)
+
+    f1 = frame(0, args.spp) * scale
+    f1b = frame(2 * world * W * H, args.spp) * scale
+    fnb = np.zeros_like(f1)
+    for g in range(world):
+        fnb += frame((world + g) * W * H, share_spp(g))
+    fnb *= scale
     fn = lin_n.astype(np.float64).reshape(-1, 3) * scale
-    shared = (args.spp // world + (1 if args.spp % world else 0)) / args.spp     # rank 0's share of F1's samples
+    npix = fn.shape[0]
+    shared = share_spp(0) / args.spp     # rank 0's share of F1's samples
     rms_n1 = np.sqrt(np.mean((fn - f1) ** 2, axis=0))
     rms_11 = np.sqrt(np.mean((f1b - f1) ** 2, axis=0))
     expected = rms_11 * np.sqrt(1.0 - shared)
     ratio = rms_n1 / np.maximum(expected, 1e-30)
-    npix = fn.shape[0]
-    mean_n, mean_1 = fn.mean(axis=0), f1.mean(axis=0)
 
     def z_of(a, b):
         d = a - b
@@ -765,27 +778,26 @@ def statistical_parity(lin_n, rays_n, r, scene, args, world, scale):
     def shown(f):   # writeColor: sqrt (gamma 2), clamped to [0, 0.999]
         return np.clip(np.sqrt(np.maximum(f, 0.0)), 0.0, 0.999)
 
-    z, z_ctrl = z_of(fn, f1), z_of(f1b, f1)
-    dn, d1, d1b = shown(fn), shown(f1), shown(f1b)
-    zd, zd_ctrl = z_of(dn, d1), z_of(d1b, d1)
+    dn, dnb, d1, d1b = shown(fn), shown(fnb), shown(f1), shown(f1b)
+    zd = z_of(dn, dnb)
     ok = bool(np.all((ratio >= 0.8) & (ratio <= 1.25)) and np.all(zd <= 5.0))
-    return {"against": f"the 1-GPU frame of the same seed ({args.spp} spp, subsequence family 0)",
+    rd = lambda v, k=7: [round(float(x), k) for x in v]  # noqa: E731
+    return {"against": f"the 1-GPU frame of the same seed ({args.spp} spp, subsequence family 0) per pixel; an "
+                       f"independent {world}-way frame (families {world}..{2 * world - 1}) for the frame mean",
             "kind": "statistical (SURVEY §8e): same estimator, other samples",
-            "frame_mean_per_channel": [round(float(v), 7) for v in mean_n],
-            "frame_mean_1gpu_per_channel": [round(float(v), 7) for v in mean_1],
-            "mean_diff_z": [round(float(v), 3) for v in z],
-            "mean_diff_z_two_1gpu_frames": [round(float(v), 3) for v in z_ctrl],
-            "displayed_mean_per_channel": [round(float(v), 7) for v in dn.mean(axis=0)],
-            "displayed_mean_1gpu_per_channel": [round(float(v), 7) for v in d1.mean(axis=0)],
-            "displayed_mean_diff_z": [round(float(v), 3) for v in zd],
-            "displayed_mean_diff_z_two_1gpu_frames": [round(float(v), 3) for v in zd_ctrl],
-            "rms_per_channel": [round(float(v), 7) for v in rms_n1],
-            "rms_two_1gpu_frames_per_channel": [round(float(v), 7) for v in rms_11],
-            "expected_rms_per_channel": [round(float(v), 7) for v in expected],
+            "rms_per_channel": rd(rms_n1), "rms_two_1gpu_frames_per_channel": rd(rms_11),
+            "expected_rms_per_channel": rd(expected),
             "expected_rule": f"sqrt(2) x MC noise x sqrt(1 - {shared:.4f}) (rank 0's samples are F1's first ones)",
-            "rms_over_expected": [round(float(v), 4) for v in ratio],
-            "rays_rel_diff": (rays_n - rays[0]) / rays[0], "rays_rel_diff_two_1gpu_frames": (rays[1] - rays[0]) / rays[0],
-            "pass": ok, "tolerance": "rms_over_expected in [0.8, 1.25], displayed_mean_diff_z <= 5"}
+            "rms_over_expected": rd(ratio, 4),
+            "frame_mean_per_channel": rd(fn.mean(axis=0)), "frame_mean_other_nway_per_channel": rd(fnb.mean(axis=0)),
+            "frame_mean_1gpu_per_channel": rd(f1.mean(axis=0)),
+            "displayed_mean_diff_z": rd(zd, 3), "mean_diff_z": rd(z_of(fn, fnb), 3),
+            "info_mean_diff_z_vs_1gpu": rd(z_of(fn, f1), 3), "info_displayed_mean_diff_z_vs_1gpu": rd(z_of(dn, d1), 3),
+            "info_mean_diff_z_two_1gpu_frames": rd(z_of(f1b, f1), 3),
+            "rays_rel_diff_vs_other_nway": (rays_n - sum(rays[2:])) / sum(rays[2:]),
+            "rays_rel_diff_vs_1gpu": (rays_n - rays[0]) / rays[0],
+            "pass": ok, "tolerance": "rms_over_expected in [0.8, 1.25]; displayed_mean_diff_z (vs the other N-way frame) "
+                                     "<= 5"}
 
 
 if __name__ == "__main__":
