@@ -300,6 +300,14 @@ def kernel_source_sha() -> str:
     return hashlib.sha256((REPO / "raytracer-cuda_amd" / "csrc" / "crt_hip.hip").read_bytes()).hexdigest()
 
 
+def kernel_library_sha() -> str | None:
+    """sha256 of the libcrt_hip.so this process renders with (CRT_HIP_LIB or the in-tree build)."""
+    import hashlib
+    from crt_amd import _lib
+    p = Path(_lib.HIP_LIB)
+    return hashlib.sha256(p.read_bytes()).hexdigest() if p.exists() else None
+
+
 def roofline_counters(key: str, kname: str, fallback_key: str | None = None):
     """The committed PMC summary of this workload (tools/pmc_summary.py), if its kernel matches: (entry, rule).
 
@@ -368,7 +376,10 @@ def roofline_from_counters(e, rays: int, kernel_s: float, algorithmic_ops: int |
                                            "tcp_pending_stall_frac", "wave_frac_waiting_memory", "l2_hit_rate")
                          if k in d},
             "counters_source": e["source"], "counters_clock_ghz": e["clock_ghz"],
-            "counters_kernel_source_current": e.get("kernel_source_sha256") == kernel_source_sha()}
+            "counters_kernel_source_current": e.get("kernel_source_sha256") == kernel_source_sha(),
+            # the library the counters were collected with is the one rendering now (source edits under profiling
+            # switches leave the shipped library byte-identical)
+            "counters_kernel_library_current": e.get("kernel_library_sha256") == kernel_library_sha()}
 
 
 def main(argv=None):

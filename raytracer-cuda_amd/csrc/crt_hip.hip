@@ -112,10 +112,20 @@ __device__ __forceinline__ uint64_t shader_clock() { return __builtin_amdgcn_s_m
 // the counting kernel keeps (s_memtime per section) also in the timed kernel, with the regeneration pass split into
 // its parts.  g_pass_prof, summed over variant 8's waves: [0] step, [1] rounds, [2] pass total, [3] finish_ray (spheres
 // + shade), [4] of which the per-ray spheres, [5] next_ray, [6] new-ray set-up (1/d, rows, LDS ray record), [7] the
-// LDS root step (top_steps), [8] loop head (live / parked ballots, the drain rule), [9] passes, [10] waves
+// LDS root step (top_steps), [8] loop head (live / parked ballots, the drain rule), [9] passes, [10] waves, [11] wave
+// lifetime (first to last instruction), [12] node steps, [13] leaf rounds, [14] rays.  -DCRT_PROFILE_PASS_FIRST=K keeps
+// only the first K workgroups of the tile order (K = 1: the most expensive tile, config B's critical chain)
+// a 64-bit value of one lane, to every lane (the profiling builds' timer accumulators)
+__device__ __forceinline__ uint64_t bcast64(uint64_t v, int lane) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), lane) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+}
 #ifdef CRT_PROFILE_PASS
 constexpr bool kProfilePass = true;
-__device__ unsigned long long g_pass_prof[12];
+__device__ unsigned long long g_pass_prof[16];
+#ifndef CRT_PROFILE_PASS_FIRST
+#define CRT_PROFILE_PASS_FIRST 0x7fffffff
+#endif
 #else
 constexpr bool kProfilePass = false;
 #endif
@@ -591,7 +601,7 @@ __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, 
     }
     uint32_t carry = 0;   // owner + 1 of the last pair of the previous round
     for (int base = 0; base < total; base += 64) {
-        if (COUNT) cnt.round_slots++;
+        if (COUNT || kProfilePass) cnt.round_slots++;
         if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)(lane + 1);
         wave_sync();
         const uint32_t mark = L.owner_at[lane];
@@ -988,7 +998,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
                                                float& closest, int& hit, TraceCounts& cnt, WaveLdsWide& L,
                                                uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix) {
     constexpr bool TIME = COUNT || kProfilePass;
-    if (COUNT) cnt.step_slots++;
+    if (COUNT || kProfilePass) cnt.step_slots++;
     const uint64_t c0 = TIME ? shader_clock() : 0;
     int leaf_n, leaf_first;
     node_step4<COUNT>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
@@ -1025,7 +1035,7 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
     }
     uint32_t carry = 0;   // owner + 1 of the last pair of the previous round
     for (int base = 0; base < total; base += 64) {
-        if (COUNT) cnt.round_slots++;
+        if (COUNT || kProfilePass) cnt.round_slots++;
         if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)(lane + 1);
         wave_sync();
         const uint32_t mark = L.owner_at[lane];
@@ -1397,6 +1407,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
 #ifdef CRT_PROFILE_WAVE_TIMES
     const unsigned long long prof_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef CRT_PROFILE_PASS
+    const uint64_t prof_life0 = shader_clock();
+#endif
     constexpr int WGW = KernelShape<VARIANT>::waves;
     // variant 4: 16 LDS stack entries per lane at 5 waves/SIMD; 12 at 6+ so 6 workgroups fit the 160 KiB
     constexpr bool PERSIST = VARIANT == 7;
@@ -1722,6 +1735,18 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 }
 #endif
                 live_mask = wave_ballot(has_result);
+                if constexpr (kProfilePass) {
+                    // the pass's section timers ran in divergent code, so each lane's accumulators hold only the passes
+                    // it took part in (lane 0 alone was reported before): every lane adopts the accumulators of a lane
+                    // that ran this pass's innermost timed section, which keeps them wave-uniform
+                    const uint64_t ran = parked_mask & live_mask;
+                    const int src = __builtin_ctzll(ran ? ran : parked_mask);
+                    cnt.cyc_shade = bcast64(cnt.cyc_shade, src);
+                    cnt.cyc_sph = bcast64(cnt.cyc_sph, src);
+                    cnt.cyc_next = bcast64(cnt.cyc_next, src);
+                    cnt.cyc_setup = bcast64(cnt.cyc_setup, src);
+                    cnt.cyc_top = bcast64(cnt.cyc_top, src);
+                }
                 first_pass = false;
                 // variant 8 counts the wave's rays in LDS (one VGPR less in the hot loop); (an LDS add without return
                 // instead of the read-modify-write measured +0.4 % on config C, profiles/r05e)
@@ -1827,10 +1852,11 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     }
     if (lane == 0) atomicAdd(&P.counters[0], (unsigned long long)wr);
 #ifdef CRT_PROFILE_PASS
-    if (!COUNT && TILED && lane == 0) {
-        const unsigned long long v[11] = {cnt.cyc_step, cnt.cyc_round, cnt.cyc_regen, cnt.cyc_shade, cnt.cyc_sph,
-                                          cnt.cyc_next, cnt.cyc_setup, cnt.cyc_top, cnt.cyc_head, cnt.passes, 1ull};
-        for (int k = 0; k < 11; ++k) atomicAdd(&g_pass_prof[k], v[k]);
+    if (!COUNT && TILED && lane == 0 && (int)blockIdx.x < CRT_PROFILE_PASS_FIRST) {
+        const unsigned long long v[15] = {cnt.cyc_step, cnt.cyc_round, cnt.cyc_regen, cnt.cyc_shade, cnt.cyc_sph,
+                                          cnt.cyc_next, cnt.cyc_setup, cnt.cyc_top, cnt.cyc_head, cnt.passes, 1ull,
+                                          shader_clock() - prof_life0, cnt.step_slots, cnt.round_slots, wave_rays};
+        for (int k = 0; k < 15; ++k) atomicAdd(&g_pass_prof[k], v[k]);
     }
 #endif
 #ifdef CRT_PROFILE_LOOPS
@@ -3941,12 +3967,12 @@ extern "C" int crt_profile_live_hist(unsigned long long* out16, int reset) {
 }
 #endif
 #ifdef CRT_PROFILE_PASS
-extern "C" int crt_profile_pass_sections(unsigned long long* out12, int reset) {
-    if (!out12) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+extern "C" int crt_profile_pass_sections(unsigned long long* out16, int reset) {
+    if (!out16) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_pass_prof), 12 * 8, 0, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_pass_prof), 16 * 8, 0, hipMemcpyDeviceToHost));
     if (reset) {
-        static const unsigned long long zero[12] = {};
+        static const unsigned long long zero[16] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pass_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice));
     }
     return CRT_OK;

@@ -50,6 +50,20 @@ def test_share_counters_fall_back_to_the_whole_frame_per_ray():
     assert bench.roofline_counters(full, "crt_render_kernel<false, 1, 1>", full) == (None, None)
 
 
+def test_counters_were_collected_with_the_in_tree_library():
+    """Every committed PMC summary names the library its passes loaded; the in-tree build must be that library, so a
+    kernel change without new PMC passes fails here instead of pricing the new kernel with the old counters."""
+    table = json.loads((REPO / "profiles" / "roofline_counters.json").read_text())
+    lib = bench.kernel_library_sha()
+    if lib is None:
+        pytest.skip("libcrt_hip.so not built")
+    for key, e in table.items():
+        assert e.get("kernel_library_sha256") == lib, key
+    e = table["cornell_bunny_2560x1440_2000spp_20b_rebuilt4"]
+    r = bench.roofline_from_counters(e, e["rays_per_launch"], e["kernel_ns_median_over_passes"] / 1e9)
+    assert r["counters_kernel_library_current"] is True
+
+
 def test_roofline_units_from_a_counter_summary():
     e = json.loads((REPO / "profiles" / "roofline_counters.json").read_text())[
         "cornell_bunny_2560x1440_2000spp_20b_rebuilt4"]

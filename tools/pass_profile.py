@@ -9,6 +9,11 @@ regeneration pass into its parts: finish_ray (the per-ray spheres, then shade), 
 rows, LDS ray record), the LDS root step (top_steps) and the rest (live mask, ray count); plus the loop head (the
 parked / live ballots and the drain rule), the node steps and the leaf rounds.  Shares of the wave cycles summed over
 waves; the timers add a few instructions per section, so the kernel is somewhat slower than the shipped one.
+
+    tools/build_profile_lib.sh passcrit -DCRT_PROFILE_PASS -DCRT_PROFILE_PASS_FIRST=1
+
+keeps only the first workgroup of the tile order, the most expensive tile: on config B (1280x720, 256 spp) its wave
+lasts the whole launch, so its iterations are the frame's critical chain.
 """
 import argparse
 import ctypes as C
@@ -36,14 +41,15 @@ hs = crt_amd.HostScene(assets.scene_files(a.scene), build_device=0)
 sc = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
 r = crt_amd.Renderer(a.w, a.h)
 r.set_camera(crt_amd.camera(a.spp))
-buf = np.zeros(12, np.uint64)
+buf = np.zeros(16, np.uint64)
 for k in range(2):   # the first frame warms up
     _lib.check(L.crt_profile_pass_sections(buf.ctypes.data_as(C.c_void_p), 1), "crt_profile_pass_sections")
     r.init_rand(41, a.base)
     r.render(sc, a.spp, 20)
     r.synchronize()
 _lib.check(L.crt_profile_pass_sections(buf.ctypes.data_as(C.c_void_p), 1), "crt_profile_pass_sections")
-step, rnd, regen, finish, sph, nxt, setup_and_next, top, head, passes, waves = (int(v) for v in buf[:11])
+step, rnd, regen, finish, sph, nxt, setup_and_next, top, head, passes, waves, life, n_steps, n_rounds, wrays = (
+    int(v) for v in buf[:15])
 setup = setup_and_next - nxt
 rest = regen - finish - nxt - setup - top
 tot = step + rnd + regen + head
@@ -51,7 +57,17 @@ rays = r.counters()["rays"]
 sh = lambda v: round(v / tot, 4)  # noqa: E731
 print(json.dumps({
     "kernel": r.last_kernel_name(), "w": a.w, "h": a.h, "spp": a.spp, "scene": a.scene, "rays": rays,
-    "main_kernel_ms": round(r.last_timings()["main_kernel_ms"], 3),
+    "main_kernel_ms": round(r.last_timings()["main_kernel_ms"], 3), "waves_profiled": waves,
+    "wave_lifetime_cycles_per_wave": round(life / max(1, waves)), "sections_over_lifetime": round(tot / max(1, life), 4),
+    "per_wave": {"iterations (node steps)": round(n_steps / max(1, waves), 1),
+                 "leaf rounds": round(n_rounds / max(1, waves), 1), "passes": round(passes / max(1, waves), 1),
+                 "rays": round(wrays / max(1, waves), 1)},
+    "cycles_per_iteration": round(tot / max(1, n_steps), 1),
+    "cycles_per_iteration_by_section": {"node step": round(step / max(1, n_steps), 1),
+                                        "leaf rounds": round(rnd / max(1, n_steps), 1),
+                                        "loop head": round(head / max(1, n_steps), 1),
+                                        "pass": round(regen / max(1, n_steps), 1)},
+    "cycles_per_leaf_round": round(rnd / max(1, n_rounds), 1),
     "wave_cycles_per_ray": round(tot / rays, 1), "passes_per_wave": round(passes / max(1, waves), 1),
     "share": {"node steps": sh(step), "leaf rounds": sh(rnd), "loop head (ballots, drain rule)": sh(head),
               "pass": sh(regen), "  per-ray spheres": sh(sph), "  shade": sh(finish - sph), "  next_ray": sh(nxt),

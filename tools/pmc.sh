@@ -10,6 +10,8 @@ shift || true
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/$OUT
 sha256sum $R/raytracer-cuda_amd/csrc/crt_hip.hip > $R/$OUT/kernel_sha.txt
+# the library the passes load (CRT_HIP_LIB or the in-tree build): bench.py checks the counters against it
+sha256sum ${CRT_HIP_LIB:-$R/raytracer-cuda_amd/lib/libcrt_hip.so} > $R/$OUT/library_sha.txt
 python3 $R/bench.py --print-workload-key "$@" > $R/$OUT/workload_key.txt
 cd /tmp && export TMPDIR=/tmp
 B="python3 $R/bench.py --steps 1 --warmup 0 --no-count --no-cpu-baseline --no-parity"

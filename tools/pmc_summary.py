@@ -86,10 +86,12 @@ def main():
             if m:
                 rays = int(m.group(1))
     sha = (Path(a.pmc_dir) / "kernel_sha.txt").read_text().split()[0] if (Path(a.pmc_dir) / "kernel_sha.txt").exists() else None
+    lib_txt = Path(a.pmc_dir) / "library_sha.txt"
+    lib_sha = lib_txt.read_text().split()[0] if lib_txt.exists() else None
     key = a.key or (Path(a.pmc_dir) / "workload_key.txt").read_text().strip()
     dur = sorted(durs)[len(durs) // 2]
     cyc = vals["GRBM_GUI_ACTIVE"] / 8
-    e = {"kernel": kname, "kernel_source_sha256": sha, "source": a.committed_dir, "rays_per_launch": rays,
+    e = {"kernel": kname, "kernel_source_sha256": sha, "kernel_library_sha256": lib_sha, "source": a.committed_dir, "rays_per_launch": rays,
          "kernel_ns_median_over_passes": dur, "clock_ghz": round(cyc / dur, 4),
          "per_launch": {k: v for k, v in sorted(vals.items())},
          "per_ray": {k: v / rays for k, v in sorted(vals.items())}}
