@@ -1397,6 +1397,13 @@ __device__ __forceinline__ void finish_ray(PathState& S, const RenderParams& P, 
 // (s_memrealtime, 100 MHz), read with crt_profile_wave_times — the occupancy timeline of the launch.
 __device__ unsigned long long g_wave_prof[2 * 4 * 65536];
 #endif
+#ifdef CRT_PROFILE_CRIT_TRACE
+// Profiling build only (tools/crit_trace.py): the first workgroup of a variant-8 launch (the most expensive tile) logs
+// s_memrealtime and its live / parked lane counts every 16 loop iterations, and every wave logs where it ran (HW_ID,
+// XCC_ID), so the critical wave's iteration rate can be set against the waves sharing its SIMD over time
+__device__ unsigned long long g_crit_trace[2 * 16384];
+__device__ unsigned g_wave_hw[2 * 4 * 65536];
+#endif
 
 // Waves per workgroup: 4 (16x16 pixels), or 1 for variant 8 (one 8x8 tile per workgroup, so a finished wave frees
 // its slot at once instead of holding it until its three siblings end).
@@ -1635,6 +1642,9 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
         const int regen_t = (TILED && (int)blockIdx.x < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
         bool first_pass = true;    // uniform
+#ifdef CRT_PROFILE_CRIT_TRACE
+        uint32_t crit_iter = 0;
+#endif
 #ifdef CRT_PROFILE_LIVE
         uint64_t lh0 = 0, lh1 = 0, lh2 = 0, lh3 = 0, lh4 = 0, lh5 = 0, lh6 = 0, lh7 = 0, lh8 = 0;
         uint64_t lt_prev = shader_clock();
@@ -1659,6 +1669,16 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                     atomicAdd(&g_live_hist[3], lh3); atomicAdd(&g_live_hist[4], lh4); atomicAdd(&g_live_hist[5], lh5);
                     atomicAdd(&g_live_hist[6], lh6); atomicAdd(&g_live_hist[7], lh7); atomicAdd(&g_live_hist[8], lh8);
                 }
+            }
+#endif
+#ifdef CRT_PROFILE_CRIT_TRACE
+            if (TILED && blockIdx.x == 0) {
+                if ((crit_iter & 15u) == 0 && (crit_iter >> 4) < 16384u && lane == 0) {
+                    g_crit_trace[2 * (crit_iter >> 4)] = __builtin_amdgcn_s_memrealtime();
+                    g_crit_trace[2 * (crit_iter >> 4) + 1] = (unsigned long long)n_live | ((unsigned long long)n_parked << 8) |
+                                                             ((unsigned long long)crit_iter << 16);
+                }
+                ++crit_iter;
             }
 #endif
             if (n_live == 0) break;
@@ -1869,6 +1889,10 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         if (lane == 0 && wid < 4u * 65536u) {
             g_wave_prof[2 * wid] = prof_t0;
             g_wave_prof[2 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+#ifdef CRT_PROFILE_CRIT_TRACE
+            g_wave_hw[2 * wid] = __builtin_amdgcn_s_getreg(4 | (31 << 11));        // HW_REG_HW_ID
+            g_wave_hw[2 * wid + 1] = __builtin_amdgcn_s_getreg(20 | (3 << 11));    // HW_REG_XCC_ID [3:0]
+#endif
         }
     }
 #endif
@@ -3987,6 +4011,19 @@ extern "C" int crt_profile_loop_counts(unsigned long long* out8, int reset) {
         static const unsigned long long zero[8] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_loop_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice));
     }
+    return CRT_OK;
+}
+#endif
+#ifdef CRT_PROFILE_CRIT_TRACE
+// out: 2 x 16384 trace words, then 2 x n_waves HW words
+extern "C" int crt_profile_crit_trace(unsigned long long* trace, unsigned* hw, int n_waves) {
+    if (!trace || !hw || n_waves <= 0 || n_waves > 4 * 65536) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(trace, HIP_SYMBOL(g_crit_trace), sizeof(unsigned long long) * 2 * 16384, 0,
+                                hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_wave_hw), (size_t)n_waves * 8, 0, hipMemcpyDeviceToHost));
+    static const unsigned long long zero[2 * 16384] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_crit_trace), zero, sizeof zero, 0, hipMemcpyHostToDevice));
     return CRT_OK;
 }
 #endif
