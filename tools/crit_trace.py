@@ -29,12 +29,15 @@ ap.add_argument("--w", type=int, default=1280)
 ap.add_argument("--h", type=int, default=720)
 ap.add_argument("--spp", type=int, default=256)
 ap.add_argument("--bins", type=int, default=10)
+ap.add_argument("--occupancy", type=int, default=0, help="crt_renderer_set_occupancy_target (0 = the library's rule)")
 a = ap.parse_args()
 
 hs = crt_amd.HostScene(assets.scene_files(a.scene), build_device=0)
 sc = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
 r = crt_amd.Renderer(a.w, a.h)
 r.set_camera(crt_amd.camera(a.spp))
+if a.occupancy:
+    r.set_occupancy_target(a.occupancy)
 L = _lib.hip()
 L.crt_profile_crit_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
 L.crt_profile_wave_times.argtypes = [C.c_void_p, C.c_int]
@@ -48,6 +51,8 @@ for k in range(2):   # the first frame warms up; the trace is reset when read
     _lib.check(L.crt_profile_crit_trace(trace.ctypes.data_as(C.c_void_p), hw.ctypes.data_as(C.c_void_p), n_waves),
                "crt_profile_crit_trace")
 kname = r.last_kernel_name()
+import hashlib  # noqa: E402
+frame_hash = hashlib.sha256(r.linear().tobytes() + r.rng_state().tobytes()).hexdigest()[:16]
 assert "8," in kname, kname
 wt = np.zeros((n_waves, 2), np.uint64)
 _lib.check(L.crt_profile_wave_times(wt.ctypes.data_as(C.c_void_p), n_waves), "crt_profile_wave_times")
@@ -92,5 +97,8 @@ out = {"kernel": kname, "w": a.w, "h": a.h, "spp": a.spp, "kernel_ms": round(r.l
                                                           "end_ms": round(end[0] / 1e3, 3),
                                                           "iterations": int(it[-1]) if len(it) else 0,
                                                           "longest_wave": bool(np.argmax(end - start) == 0)},
-       "waves_sharing_its_simd": int(same_simd.sum()) - 1, "series": series}
+       "waves_sharing_its_simd": int(same_simd.sum()) - 1, "frame_and_rng_sha": frame_hash,
+       "longest_waves": [{"block": int(b), "ms": round(float(end[b] - start[b]) / 1e3, 3),
+                          "start_ms": round(float(start[b]) / 1e3, 3)} for b in np.argsort(start - end)[:8]],
+       "series": series}
 print(json.dumps(out, indent=1))
