@@ -106,6 +106,9 @@ struct TraceCounts {
     uint64_t cyc_shade, cyc_next;   // inside the regen pass: ray_spheres() + shade(), next_ray(); the rest is ray init
     uint64_t cyc_sph;               // of cyc_shade: the per-ray spheres (ray_spheres)
     uint64_t cyc_setup, cyc_top, cyc_head;   // CRT_PROFILE_PASS: new-ray set-up, LDS root step, loop head
+#ifdef CRT_PROFILE_ROWS
+    uint64_t cyc_rows, cyc_prims;            // node-row and primitive-record load-to-data cycles (profiling build)
+#endif
 };
 __device__ __forceinline__ uint64_t shader_clock() { return __builtin_amdgcn_s_memtime(); }
 // Profiling build only (tools/build_profile_lib.sh pass -DCRT_PROFILE_PASS, tools/pass_profile.py): the section timers
@@ -114,7 +117,9 @@ __device__ __forceinline__ uint64_t shader_clock() { return __builtin_amdgcn_s_m
 // + shade), [4] of which the per-ray spheres, [5] next_ray, [6] new-ray set-up (1/d, rows, LDS ray record), [7] the
 // LDS root step (top_steps), [8] loop head (live / parked ballots, the drain rule), [9] passes, [10] waves, [11] wave
 // lifetime (first to last instruction), [12] node steps, [13] leaf rounds, [14] rays.  -DCRT_PROFILE_PASS_FIRST=K keeps
-// only the first K workgroups of the tile order (K = 1: the most expensive tile, config B's critical chain)
+// only the first K workgroups of the tile order (K = 1: the most expensive tile, config B's critical chain).  With
+// -DCRT_PROFILE_ROWS as well: [15] the node step's wait for its seven rows and [16] the leaf round's wait for its
+// primitive records (the loads issued, then an explicit vmcnt(0) between two timers)
 // a 64-bit value of one lane, to every lane (the profiling builds' timer accumulators)
 __device__ __forceinline__ uint64_t bcast64(uint64_t v, int lane) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), lane) << 32) |
@@ -122,7 +127,7 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t v, int lane) {
 }
 #ifdef CRT_PROFILE_PASS
 constexpr bool kProfilePass = true;
-__device__ unsigned long long g_pass_prof[16];
+__device__ unsigned long long g_pass_prof[20];
 #ifndef CRT_PROFILE_PASS_FIRST
 #define CRT_PROFILE_PASS_FIRST 0x7fffffff
 #endif
@@ -709,12 +714,18 @@ __device__ __forceinline__ uint32_t sign_row(float inv) { return (__float_as_uin
 __device__ __forceinline__ uint32_t ray_rows(V3 inv) {
     return sign_row(inv.x) | ((32u ^ sign_row(inv.y)) << 8) | ((64u ^ sign_row(inv.z)) << 16);
 }
+__device__ __forceinline__ Wide4 wide_boxes_of(const float4& nxr, const float4& fxr, const float4& nyr, const float4& fyr,
+                                               const float4& nzr, const float4& fzr, V3 o, V3 inv, float tmax);
 __device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ nodes, uint32_t b, uint32_t rows, V3 o, V3 inv,
                                             float tmax) {
     const uint32_t ex = b ^ (rows & 0xffu), ey = b ^ ((rows >> 8) & 0xffu), ez = b ^ (rows >> 16);
     const float4 nxr = *rec_at(nodes, ex), fxr = *rec_at(nodes, ex ^ 16u);
     const float4 nyr = *rec_at(nodes, ey), fyr = *rec_at(nodes, ey ^ 16u);
     const float4 nzr = *rec_at(nodes, ez), fzr = *rec_at(nodes, ez ^ 16u);
+    return wide_boxes_of(nxr, fxr, nyr, fyr, nzr, fzr, o, inv, tmax);
+}
+__device__ __forceinline__ Wide4 wide_boxes_of(const float4& nxr, const float4& fxr, const float4& nyr, const float4& fyr,
+                                               const float4& nzr, const float4& fzr, V3 o, V3 inv, float tmax) {
     // one v_fma_f32 per plane: a v_pk_fma_f32 costs the SIMD the same cycles as two (MI355X_MICROARCH.md) and needs
     // {inv, inv} / {-o*inv, -o*inv} register pairs, which made the persistent variant 7 spill in this step (the
     // scalar form: variant 8 -1.7 %, variant 7 -18 %, profiles/r02aa)
@@ -914,10 +925,27 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
                                            size_t n_pix, int& leaf_first, int& leaf_n) {
     leaf_n = 0;
     leaf_first = 0;
+#ifdef CRT_PROFILE_ROWS
+    uint64_t row_wait = 0;
+#endif
     if (node >= 0) {
         const uint32_t b = node_base(node);
+#ifdef CRT_PROFILE_ROWS
+        // profiling build: the seven rows issued, then waited for between two timers
+        const uint32_t ex = b ^ (rows & 0xffu), ey = b ^ ((rows >> 8) & 0xffu), ez = b ^ (rows >> 16);
+        const uint64_t ra = shader_clock();
+        const float4 mf = node_row(P.nodes, b, 6);
+        const float4 nxr = *rec_at(P.nodes, ex), fxr = *rec_at(P.nodes, ex ^ 16u);
+        const float4 nyr = *rec_at(P.nodes, ey), fyr = *rec_at(P.nodes, ey ^ 16u);
+        const float4 nzr = *rec_at(P.nodes, ez), fzr = *rec_at(P.nodes, ez ^ 16u);
+        __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
+        __asm__ volatile("" : : "v"(mf.x), "v"(nxr.x), "v"(fxr.x), "v"(nyr.x), "v"(fyr.x), "v"(nzr.x), "v"(fzr.x) : "memory");
+        row_wait = shader_clock() - ra;
+        const Wide4 w = wide_boxes_of(nxr, fxr, nyr, fyr, nzr, fzr, o, inv, closest);
+#else
         const float4 mf = node_row(P.nodes, b, 6);
         const Wide4 w = wide_boxes(P.nodes, b, rows, o, inv, closest);
+#endif
         // keep the whole link row in the node's loads: left to itself the compiler loads leaf_first / counts
         // only inside the leaf branch, one more dependent load on a leaf step's critical path.  Pinned after the
         // box tests, so the wait it implies is the one the boxes need anyway (pinned before them, it made the six
@@ -991,6 +1019,12 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
             node = -1;
         }
     }
+#ifdef CRT_PROFILE_ROWS
+    {   // the wait of a lane that stepped (uniform among them: the timers are scalar)
+        const uint64_t st = wave_ballot(row_wait != 0);
+        if (st) cnt.cyc_rows += bcast64(row_wait, __builtin_ctzll(st));
+    }
+#endif
 }
 
 template <bool COUNT>
@@ -1043,11 +1077,25 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         const uint32_t owner1 = max(wave_inclusive_max_scan_u(mark), carry);
         const int owner = (int)owner1 - 1;
         const int j = base + lane;
+#ifdef CRT_PROFILE_ROWS
+        uint64_t prim_wait = 0;
+#endif
         if (j < total) {
             const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
             const int p = __float_as_int(r1.w) + j;   // leaf_first - prefix + j: inside the owner's checked span
             if (COUNT) cnt.tris++;
             int rank;
+#ifdef CRT_PROFILE_ROWS
+            {   // profiling build: the pair's record loaded and waited for between two timers (prim_test reloads it
+                // from the vector L1)
+                const float4* rr = rec_at(P.prims, __umul24((uint32_t)p, 48u));
+                const uint64_t pa = shader_clock();
+                const float4 g0 = rr[0], g1 = rr[1], g2 = rr[2];
+                __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
+                __asm__ volatile("" : : "v"(g0.x), "v"(g1.x), "v"(g2.x) : "memory");
+                prim_wait = shader_clock() - pa;
+            }
+#endif
 #ifdef CRT_CHECKED
             // checked build (-DCRT_CHECKED, lib/checked/): the per-pair bounds the fast path proves once per lane and
             // step (node_step4), re-checked here with the owner lookup itself, so a stale LDS owner mark or a wrong
@@ -1067,6 +1115,9 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
             const unsigned long long kp = ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank);
             atomicMin(&L.key[owner], t >= 0.f ? kp : ~0ull);
         }
+#ifdef CRT_PROFILE_ROWS
+        cnt.cyc_prims += bcast64(prim_wait, 0);   // lane 0's slot base + 0 < total is always tested
+#endif
         carry = __builtin_amdgcn_readlane(owner1, 63);
         wave_sync();
     }
@@ -1873,10 +1924,16 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
     if (lane == 0) atomicAdd(&P.counters[0], (unsigned long long)wr);
 #ifdef CRT_PROFILE_PASS
     if (!COUNT && TILED && lane == 0 && (int)blockIdx.x < CRT_PROFILE_PASS_FIRST) {
-        const unsigned long long v[15] = {cnt.cyc_step, cnt.cyc_round, cnt.cyc_regen, cnt.cyc_shade, cnt.cyc_sph,
+        const unsigned long long v[17] = {cnt.cyc_step, cnt.cyc_round, cnt.cyc_regen, cnt.cyc_shade, cnt.cyc_sph,
                                           cnt.cyc_next, cnt.cyc_setup, cnt.cyc_top, cnt.cyc_head, cnt.passes, 1ull,
-                                          shader_clock() - prof_life0, cnt.step_slots, cnt.round_slots, wave_rays};
-        for (int k = 0; k < 15; ++k) atomicAdd(&g_pass_prof[k], v[k]);
+                                          shader_clock() - prof_life0, cnt.step_slots, cnt.round_slots, wave_rays,
+#ifdef CRT_PROFILE_ROWS
+                                          cnt.cyc_rows, cnt.cyc_prims
+#else
+                                          0ull, 0ull
+#endif
+        };
+        for (int k = 0; k < 17; ++k) atomicAdd(&g_pass_prof[k], v[k]);
     }
 #endif
 #ifdef CRT_PROFILE_LOOPS
@@ -3991,12 +4048,12 @@ extern "C" int crt_profile_live_hist(unsigned long long* out16, int reset) {
 }
 #endif
 #ifdef CRT_PROFILE_PASS
-extern "C" int crt_profile_pass_sections(unsigned long long* out16, int reset) {
-    if (!out16) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
+extern "C" int crt_profile_pass_sections(unsigned long long* out20, int reset) {
+    if (!out20) return set_error(CRT_ERR_INVALID_ARGUMENT, "bad argument");
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_pass_prof), 16 * 8, 0, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyFromSymbol(out20, HIP_SYMBOL(g_pass_prof), 20 * 8, 0, hipMemcpyDeviceToHost));
     if (reset) {
-        static const unsigned long long zero[16] = {};
+        static const unsigned long long zero[20] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pass_prof), zero, sizeof zero, 0, hipMemcpyHostToDevice));
     }
     return CRT_OK;

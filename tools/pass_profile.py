@@ -41,15 +41,15 @@ hs = crt_amd.HostScene(assets.scene_files(a.scene), build_device=0)
 sc = hs.upload(0, bvh="rebuilt", width=4, leaf_size=4, traversal_cost=2.0, gpu_build=True)
 r = crt_amd.Renderer(a.w, a.h)
 r.set_camera(crt_amd.camera(a.spp))
-buf = np.zeros(16, np.uint64)
+buf = np.zeros(20, np.uint64)
 for k in range(2):   # the first frame warms up
     _lib.check(L.crt_profile_pass_sections(buf.ctypes.data_as(C.c_void_p), 1), "crt_profile_pass_sections")
     r.init_rand(41, a.base)
     r.render(sc, a.spp, 20)
     r.synchronize()
 _lib.check(L.crt_profile_pass_sections(buf.ctypes.data_as(C.c_void_p), 1), "crt_profile_pass_sections")
-step, rnd, regen, finish, sph, nxt, setup_and_next, top, head, passes, waves, life, n_steps, n_rounds, wrays = (
-    int(v) for v in buf[:15])
+step, rnd, regen, finish, sph, nxt, setup_and_next, top, head, passes, waves, life, n_steps, n_rounds, wrays, \
+    row_wait, prim_wait = (int(v) for v in buf[:17])
 setup = setup_and_next - nxt
 rest = regen - finish - nxt - setup - top
 tot = step + rnd + regen + head
@@ -68,6 +68,9 @@ print(json.dumps({
                                         "loop head": round(head / max(1, n_steps), 1),
                                         "pass": round(regen / max(1, n_steps), 1)},
     "cycles_per_leaf_round": round(rnd / max(1, n_rounds), 1),
+    # -DCRT_PROFILE_ROWS builds only (0 otherwise): the loads' issue-to-data cycles, per node step / leaf round
+    "row_wait_cycles_per_iteration": round(row_wait / max(1, n_steps), 1),
+    "prim_wait_cycles_per_leaf_round": round(prim_wait / max(1, n_rounds), 1),
     "wave_cycles_per_ray": round(tot / rays, 1), "passes_per_wave": round(passes / max(1, waves), 1),
     "share": {"node steps": sh(step), "leaf rounds": sh(rnd), "loop head (ballots, drain rule)": sh(head),
               "pass": sh(regen), "  per-ray spheres": sh(sph), "  shade": sh(finish - sph), "  next_ray": sh(nxt),
