@@ -724,6 +724,15 @@ __device__ __forceinline__ Wide4 wide_boxes(const float4* __restrict__ nodes, ui
     const float4 nzr = *rec_at(nodes, ez), fzr = *rec_at(nodes, ez ^ 16u);
     return wide_boxes_of(nxr, fxr, nyr, fyr, nzr, fzr, o, inv, tmax);
 }
+// The rows of node b for the row prefetch of variant 8 at occupancy 4 (traverse_step4<.., true>): pf[0..5] = the ray's
+// entry / exit rows per axis (the order wide_boxes_of takes), pf[6] = the link row.
+__device__ __forceinline__ void load_node_rows(const float4* __restrict__ nodes, uint32_t b, uint32_t rows, float4* pf) {
+    const uint32_t ex = b ^ (rows & 0xffu), ey = b ^ ((rows >> 8) & 0xffu), ez = b ^ (rows >> 16);
+    pf[0] = *rec_at(nodes, ex); pf[1] = *rec_at(nodes, ex ^ 16u);
+    pf[2] = *rec_at(nodes, ey); pf[3] = *rec_at(nodes, ey ^ 16u);
+    pf[4] = *rec_at(nodes, ez); pf[5] = *rec_at(nodes, ez ^ 16u);
+    pf[6] = *rec_at(nodes, b ^ (6u << 4));
+}
 __device__ __forceinline__ Wide4 wide_boxes_of(const float4& nxr, const float4& fxr, const float4& nyr, const float4& fyr,
                                                const float4& nzr, const float4& fzr, V3 o, V3 inv, float tmax) {
     // one v_fma_f32 per plane: a v_pk_fma_f32 costs the SIMD the same cycles as two (MI355X_MICROARCH.md) and needs
@@ -919,10 +928,11 @@ __device__ __forceinline__ int lane_fresh() {
     return l;
 }
 
-template <bool COUNT>
+template <bool COUNT, bool PF = false>
 __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, uint32_t rows, int& node, int& sp, float closest,
                                            TraceCounts& cnt, uint32_t* __restrict__ stk, int lane, size_t pix,
-                                           size_t n_pix, int& leaf_first, int& leaf_n) {
+                                           size_t n_pix, int& leaf_first, int& leaf_n, float4* pf = nullptr,
+                                           bool have_pf = false) {
     leaf_n = 0;
     leaf_first = 0;
 #ifdef CRT_PROFILE_ROWS
@@ -943,8 +953,12 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
         row_wait = shader_clock() - ra;
         const Wide4 w = wide_boxes_of(nxr, fxr, nyr, fyr, nzr, fzr, o, inv, closest);
 #else
-        const float4 mf = node_row(P.nodes, b, 6);
-        const Wide4 w = wide_boxes(P.nodes, b, rows, o, inv, closest);
+        // PF: the rows are in pf when the previous step's first leaf round loaded them for this node (have_pf), else
+        // they load here as without the prefetch
+        if (PF && !have_pf) load_node_rows(P.nodes, b, rows, pf);
+        const float4 mf = PF ? pf[6] : node_row(P.nodes, b, 6);
+        const Wide4 w = PF ? wide_boxes_of(pf[0], pf[1], pf[2], pf[3], pf[4], pf[5], o, inv, closest)
+                           : wide_boxes(P.nodes, b, rows, o, inv, closest);
 #endif
         // keep the whole link row in the node's loads: left to itself the compiler loads leaf_first / counts
         // only inside the leaf branch, one more dependent load on a leaf step's critical path.  Pinned after the
@@ -1027,14 +1041,21 @@ __device__ __forceinline__ void node_step4(const RenderParams& P, V3 o, V3 inv, 
 #endif
 }
 
-template <bool COUNT>
+template <bool COUNT, bool PF = false>
 __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d, V3 inv, uint32_t rows, int& node, int& sp,
                                                float& closest, int& hit, TraceCounts& cnt, WaveLdsWide& L,
-                                               uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix) {
+                                               uint32_t* __restrict__ stk, int lane, size_t pix, size_t n_pix,
+                                               float4* pf = nullptr, int* pf_node = nullptr) {
     constexpr bool TIME = COUNT || kProfilePass;
     if (COUNT || kProfilePass) cnt.step_slots++;
     const uint64_t c0 = TIME ? shader_clock() : 0;
     int leaf_n, leaf_first;
+    if constexpr (PF) {
+        // pf holds node *pf_node's rows when the previous step's first leaf round loaded them (profiles/r06r)
+        node_step4<COUNT, true>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n, pf,
+                                *pf_node == node);
+        *pf_node = -1;
+    } else
     node_step4<COUNT>(P, o, inv, rows, node, sp, closest, cnt, stk, lane, pix, n_pix, leaf_first, leaf_n);
     const uint64_t c1 = TIME ? shader_clock() : 0;
     if (TIME) cnt.cyc_step += c1 - c0;
@@ -1068,6 +1089,57 @@ __device__ __forceinline__ void traverse_step4(const RenderParams& P, V3 o, V3 d
         L.key[lane] = ((unsigned long long)ones << 32) | ones;
     }
     uint32_t carry = 0;   // owner + 1 of the last pair of the previous round
+    if constexpr (PF) {
+        // The row prefetch (variant 8 at occupancy 4, profiles/r06r): the lane's next node is known before the leaf
+        // rounds, and their hits only lower `closest`, which the rows do not depend on.  The first round loads every
+        // lane's pair record (slots past the end: record 0), THEN the lane's next node's seven rows (node 0 for a lane
+        // without one): vector-memory loads retire in order, so the round waits for its records only (rows loaded
+        // before the records made the round wait for them too: +3.6 %, profiles/r06o).  The next node step finds the
+        // rows in registers (28 VGPRs, which is why this needs occupancy 4's budget).
+        auto round = [&](int base, auto first) {
+            if (COUNT || kProfilePass) cnt.round_slots++;
+            if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)(lane + 1);
+            wave_sync();
+            const uint32_t mark = L.owner_at[lane];
+            L.owner_at[lane] = 0;
+            const uint32_t owner1 = max(wave_inclusive_max_scan_u(mark), carry);
+            const int owner = (int)owner1 - 1;   // >= 0 on every lane: slot 0 of round 0 carries a mark
+            const int j = base + lane;
+            const float4 r0 = L.ray0[owner], r1 = L.ray1[owner];
+#ifdef CRT_CHECKED
+            // checked build: the fast path's per-pair bounds re-checked, as in the rounds below
+            const bool bad = j < total && ((unsigned)owner >= 64u || j < L.prefix[owner] ||
+                                           j >= L.prefix[owner] + L.span_n[owner] ||
+                                           (unsigned)(__float_as_int(r1.w) + j) >= (unsigned)P.n_prims);
+            if (bad) atomicOr(P.err, 4u);
+            const bool act = j < total && !bad;
+#else
+            const bool act = j < total;
+#endif
+            const int pp = act ? __float_as_int(r1.w) + j : 0;
+            const float4* rr = rec_at(P.prims, __umul24((uint32_t)pp, 48u));
+            const float4 f0 = rr[0], f1 = rr[1], f2 = rr[2];
+            if constexpr (decltype(first)::value) {
+                __asm__ volatile("" : : : "memory");   // the rows after the records
+                load_node_rows(P.nodes, node_base(node >= 0 ? node : 0), rows, pf);
+            }
+            if (act) {
+                if (COUNT) cnt.tris++;
+                __asm__ volatile("" : : "v"(f2.y));   // the third row as one dwordx4 (prim_test)
+                const V3 ro = v3(r0.x, r0.y, r0.z), rd = v3(r0.w, r1.x, r1.y);
+                const int rank = __float_as_int(f2.z);
+                const float t = (P.tree_spheres != 0 && __float_as_int(f2.w) == 1) ? sphere_candidate(f0, f1, ro, rd, r1.z)
+                                                                                  : tri_test_flat(f0, f1, f2, ro, rd, r1.z);
+                const unsigned long long kp = ((unsigned long long)__float_as_uint(t) << 32) | (0xffffffffu - (unsigned)rank);
+                atomicMin(&L.key[owner], t >= 0.f ? kp : ~0ull);
+            }
+            carry = __builtin_amdgcn_readlane(owner1, 63);
+            wave_sync();
+        };
+        round(0, std::true_type{});
+        *pf_node = node;
+        for (int base = 64; base < total; base += 64) round(base, std::false_type{});
+    } else
     for (int base = 0; base < total; base += 64) {
         if (COUNT || kProfilePass) cnt.round_slots++;
         if (leaf_n > 0 && pfx >= base && pfx < base + 64) L.owner_at[pfx - base] = (unsigned char)(lane + 1);
@@ -1693,6 +1765,11 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
         // (their pixels' sample chains are sequential); they regenerate sooner (profiles/r02h)
         const int regen_t = (TILED && (int)blockIdx.x < P.crit_tiles) ? P.crit_threshold : P.regen_threshold;
         bool first_pass = true;    // uniform
+        // variant 8 at occupancy 4 (frames of few tiles per wave slot, bound by their most expensive tiles' sample
+        // chains): the next node's rows load during the leaf round (traverse_step4<.., true>, profiles/r06r, r06s)
+        constexpr bool PFV = TILED && MINW <= 4;
+        float4 pf[PFV ? 7 : 1];
+        int pf_node = -1;   // the node whose rows pf holds
 #ifdef CRT_PROFILE_CRIT_TRACE
         uint32_t crit_iter = 0;
 #endif
@@ -1824,6 +1901,10 @@ __global__ __launch_bounds__(64 * KernelShape<VARIANT>::waves, MINW) void crt_re
                 if (TILED && lane == 0) L.rays += (uint32_t)__popcll(parked_mask & live_mask);
             }
             if (TIME) cnt.cyc_regen += shader_clock() - c0;
+            if constexpr (PFV) {
+                traverse_step4<COUNT, true>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix,
+                                            n_pix, pf, &pf_node);
+            } else
             traverse_step4<COUNT>(P, S.o, S.d, inv, rows, node, sp, closest, hit, cnt, L, stk, lane, (size_t)pix, n_pix);
         }
     } else if constexpr (VARIANT == 2 || VARIANT == 3 || VARIANT == 10) {
@@ -3596,15 +3677,23 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     if (S->width != 4 && !(tv >= 0 && tv <= 3) && tv != 10) tv = probe_spp_for(R, spp) > 0 ? 10 : 3;
     // occupancy target (waves per SIMD): variant 8 runs at 7 (72 VGPRs, 8 LDS stack entries so that 28 one-wave
     // workgroups fit a CU's LDS; -2.4 % on config C, profiles/r03aj) when its frame has at least 4 tiles per wave slot,
-    // else at 6: a frame with few tiles per slot ends with its most expensive tile's sequential sample chain, which a
-    // seventh wave per SIMD slows down (config B, 2 tiles per slot: +3.3 % at 7, profiles/r03ak).  The other 4-wide
-    // variants run at 6, threaded scenes at 5.
+    // else at 6, or at 4 with the row prefetch when even 4 waves per SIMD leave fewer than 4.25 tiles per slot: a frame with
+    // few tiles per slot ends with its most expensive tiles' sequential sample chains (config B, 2 tiles per slot: +3.3 %
+    // at 7, profiles/r03ak), and the prefetch takes the node rows' wait off every iteration of a chain (B -8 % against
+    // occupancy 6, profiles/r06r, r06s, r06t; with more tiles the lost waves cost more: 1600x900 +18 %, C +24 %).  The
+    // other 4-wide variants run at 6, threaded scenes at 5.
     // Variants 10 and 3 (threaded, bit-exact) run at 6 (80 VGPRs; -8.0 % and -4.8 % against 5, profiles/r03am, r03as).
     int occ = R->min_waves ? R->min_waves : (S->width == 4 || tv == 10 || tv == 3 ? 6 : 5);
     if (!R->min_waves && S->width == 4 && (wv == 8 || R->tile_shards > 1)) {
         if (!R->n_cus) HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
         const size_t tiles = (size_t)((R->width + 7) / 8) * ((R->height + 7) / 8) / (size_t)std::max(1, R->tile_shards);
-        if (tiles >= (size_t)4 * R->n_cus * 4 * 7) occ = 7;
+        // at least 4 tiles per wave slot: occupancy 7 (throughput); fewer than 4.25 per slot even at occupancy 4: the
+        // frame ends with its most expensive tiles' sample chains, which the row prefetch of occupancy 4 shortens (at 256
+        // spp, against occupancy 6: 3.5 tiles per slot (config B) -8 %, 3.9 -7 %, 4.0 -6 %, 4.5 +2 %, 5.5 +18 %; a
+        // 2000-spp pixel shard at 1.8 per slot -6.5 %; profiles/r06t, r06u); in between, 6.  (The counting kernel keeps
+        // 6: its counts do not depend on the schedule.)
+        const size_t slots4 = (size_t)4 * R->n_cus * 4;
+        occ = tiles >= (size_t)4 * R->n_cus * 4 * 7 ? 7 : (4 * tiles < 17 * slots4 && !cnt) ? 4 : 6;
     }
     P.stack_lds = std::min(R->stack_lds, occ >= 7 ? CRT_STACK7 : occ >= 6 ? CRT_STACK6 : STACK_LDS);
     // a stack_cap override below the LDS entries must still report the entries it drops (crt_scene_options.stack_cap)
@@ -3696,6 +3785,9 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 8, 6>", cs);
             if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 8, 6>), tgrid, tblock, 0, st, P);
             else hipLaunchKernelGGL((crt_render_kernel<false, 8, 6>), tgrid, tblock, 0, st, P);
+        } else if (occ <= 4 && !cnt) {   // with the row prefetch (profiles/r06r, r06s); the counting kernel runs at 5
+            std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<false, 8, 4>");
+            hipLaunchKernelGGL((crt_render_kernel<false, 8, 4>), tgrid, tblock, 0, st, P);
         } else {
             std::snprintf(R->kernel_name, sizeof R->kernel_name, "crt_render_kernel<%s, 8, 5>", cs);
             if (cnt) hipLaunchKernelGGL((crt_render_kernel<true, 8, 5>), tgrid, tblock, 0, st, P);

@@ -90,7 +90,7 @@ def test_variant8_probe_schedule_against_oracle(oracle_scenes, device_scenes):
     r.init_rand(41)
     r.render(sc, spp, 20)
     r.synchronize()
-    assert r.last_kernel_name() == "crt_render_kernel<false, 8, 6>"
+    assert r.last_kernel_name() == "crt_render_kernel<false, 8, 4>"
     lin = r.linear()
     o_sum, _, o_cnt = oracle_scenes["cornell_bunny"].render(crt_amd.camera_floats(cam), w, h, spp, 20)
     rms = np.sqrt(np.mean(((lin - o_sum) / spp).astype(np.float64) ** 2, axis=(0, 1)))

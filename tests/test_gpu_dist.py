@@ -148,7 +148,7 @@ def test_pixel_shards_equal_the_one_gpu_frame(tmp_path, world):
     r.render(sc, spp, 20)
     r.resolve(crt_amd.pixel_sample_scale(spp))
     r.synchronize()
-    assert r.last_kernel_name() == "crt_render_kernel<false, 8, 6>"
+    assert r.last_kernel_name() == "crt_render_kernel<false, 8, 4>"
     assert np.array_equal(got["lin"].view(np.uint32), r.linear().view(np.uint32))
     assert np.array_equal(got["rgba"], r.rgba8())
 

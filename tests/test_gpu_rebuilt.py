@@ -264,12 +264,13 @@ def test_top_levels_rejects_bad_arguments():
 
 
 def test_occupancy_seven_is_bit_identical_and_automatic(rebuilt):
-    """Variant 8 at 7 waves/SIMD (8 LDS stack entries, deeper entries in HBM) renders the occupancy-6 frame bit for bit;
-    the automatic choice takes 7 for a headline-sized frame (>= 4 tiles per wave slot) and 6 for a small one."""
+    """Variant 8 at 7 waves/SIMD (8 LDS stack entries, deeper entries in HBM) and at 4 (16 entries, the next node's rows
+    loaded during the leaf round) render the occupancy-6 frame bit for bit; the automatic choice takes 7 for a
+    headline-sized frame (>= 4 tiles per wave slot) and 4 for a small one."""
     dev = rebuilt["cornell_bunny", "w4"]
     w, h, spp = 2560, 1440, 64
     out = []
-    for occ in (6, 0):
+    for occ in (6, 0, 4):
         r = crt_amd.Renderer(w, h)
         if occ:
             r.set_occupancy_target(occ)
@@ -278,11 +279,33 @@ def test_occupancy_seven_is_bit_identical_and_automatic(rebuilt):
         r.render(dev, spp, 20)
         r.synchronize()
         out.append((r.last_kernel_name(), r.linear().view(np.uint32), r.rng_state(), r.counters()["rays"]))
-    (k6, lin6, rng6, rays6), (k7, lin7, rng7, rays7) = out
+    (k6, lin6, rng6, rays6), (k7, lin7, rng7, rays7), (k4, lin4, rng4, rays4) = out
     assert k6 == "crt_render_kernel<false, 8, 6>" and k7 == "crt_render_kernel<false, 8, 7>"
+    assert k4 == "crt_render_kernel<false, 8, 4>"
     assert np.array_equal(lin6, lin7) and np.array_equal(rng6, rng7) and rays6 == rays7
+    assert np.array_equal(lin6, lin4) and np.array_equal(rng6, rng4) and rays6 == rays4
     small = _frame(dev, 104, 45, 64, 20, crt_amd.camera(64), variant=-1)
-    assert small.last_kernel_name() == "crt_render_kernel<false, 8, 6>"
+    assert small.last_kernel_name() == "crt_render_kernel<false, 8, 4>"
+
+
+@pytest.mark.parametrize("scene,w,h,spp", [("cornell_bunny", 100, 37, 70), ("cornell_bunny", 1280, 720, 64),
+                                           ("cornell_1m", 320, 180, 64)])
+def test_row_prefetch_is_bit_identical(rebuilt, request, scene, w, h, spp):
+    """Variant 8 at occupancy 4 loads each lane's next node rows during the step's first leaf round and uses them in the
+    next node step (lanes given a new ray in between load their own): frames, RNG state and ray counts equal occupancy
+    6's, on a ragged frame, a config-B-sized frame and the deep 1M-triangle tree."""
+    dev = request.getfixturevalue("config_e")[0] if scene == "cornell_1m" else rebuilt[scene, "w4"]
+    out = []
+    for occ in (6, 4):
+        r = crt_amd.Renderer(w, h)
+        r.set_occupancy_target(occ)
+        r.set_camera(crt_amd.camera(spp))
+        r.init_rand(41)
+        r.render(dev, spp, 20)
+        r.synchronize()
+        out.append((r.last_kernel_name(), r.linear().view(np.uint32), r.rng_state(), r.counters()["rays"]))
+    assert out[0][0].endswith("8, 6>") and out[1][0].endswith("8, 4>")
+    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2]) and out[0][3] == out[1][3]
 
 
 def _usable_cores() -> int:
@@ -390,12 +413,12 @@ BANDS_B_FULL = (4, 352, 488, 716)      # full-width 4-row bands of config B; y0 
 
 
 def test_config_b_shipped_instantiation_against_the_oracle(rebuilt, oracle_scenes):
-    """Config B's benchmarked kernel (1280x720, 256 spp: 2 tiles per wave slot, so crt_render_kernel<false, 8, 6>) against
+    """Config B's benchmarked kernel (1280x720, 256 spp: 2 tiles per wave slot, so crt_render_kernel<false, 8, 4>) against
     the oracle directly, not against the reference-BVH GPU frame: four full-width bands at the full 256 spp, one through
     the glass bunny, each within the north-star bar with >= 99.9 % of its pixels bit-identical."""
     dev = rebuilt["cornell_bunny", "w4"]
     w, h, spp = 1280, 720, 256
-    r, cf = _shipped_frame(dev, w, h, spp, "crt_render_kernel<false, 8, 6>")
+    r, cf = _shipped_frame(dev, w, h, spp, "crt_render_kernel<false, 8, 4>")
     lin, rgba = r.linear(), r.rgba8()
     nt = _usable_cores()
     osc = oracle_scenes["cornell_bunny"]
