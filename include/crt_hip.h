@@ -335,6 +335,11 @@ uint8_t* crt_renderer_rgba_device_ptr(crt_renderer* r);
 uint32_t* crt_renderer_rng_device_ptr(crt_renderer* r);
 /* Milliseconds of the last render kernel launch(es), measured with HIP events on the launch stream. */
 float crt_renderer_last_kernel_ms(crt_renderer* r);
+/* The occupancy choice of the last variant-8 render: out[0] = rho, the probe's largest tile work over the mean work per
+ * occupancy-6 wave slot (0 when the choice did not use the probe), out[1] = the occupancy launched (waves per SIMD; 0
+ * for other variants), out[2] = the largest tile work and out[3] = the mean tile work (probe cost units).  An
+ * extension of this port (the reference has one kernel shape), like crt_renderer_last_timings. */
+int crt_renderer_last_schedule(crt_renderer* r, float out[4]);
 /* HIP-event times of the last render, in ms: out[0] = the whole render (== crt_renderer_last_kernel_ms), out[1] = what
  * runs before the main render kernel (variant 8 / 7: the cost probe and the tile sort; 0 otherwise), out[2] = the main
  * render kernel alone. */

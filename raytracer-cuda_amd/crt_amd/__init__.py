@@ -303,6 +303,14 @@ class Renderer:
     def last_kernel_name(self) -> str:
         return (_lib.hip().crt_renderer_last_kernel_name(self.h) or b"").decode()
 
+    def last_schedule(self) -> dict:
+        """The last variant-8 render's occupancy choice (crt_renderer_last_schedule): rho = the probe's largest tile work
+        over the mean work per occupancy-6 wave slot (0 without the probe-based choice), the occupancy launched, and the
+        largest and mean tile works."""
+        a = (C.c_float * 4)()
+        check(_lib.hip().crt_renderer_last_schedule(self.h, a), "last_schedule")
+        return {"rho": a[0], "occupancy": int(a[1]), "max_tile_work": a[2], "mean_tile_work": a[3]}
+
     def last_timings(self) -> dict:
         """HIP-event ms of the last render: the whole render, the probe + tile sort before the main kernel, and the
         main render kernel alone (crt_renderer_last_timings)."""

@@ -103,7 +103,7 @@ HIP_SYMBOLS = [
     "crt_renderer_synchronize", "crt_renderer_read_linear", "crt_renderer_read_rgba8", "crt_renderer_read_rng",
     "crt_renderer_write_linear", "crt_renderer_get_counters", "crt_renderer_linear_device_ptr",
     "crt_renderer_rgba_device_ptr", "crt_renderer_rng_device_ptr", "crt_renderer_last_kernel_ms",
-    "crt_renderer_last_kernel_name", "crt_renderer_last_timings", "crt_renderer_timing_history",
+    "crt_renderer_last_kernel_name", "crt_renderer_last_timings", "crt_renderer_last_schedule", "crt_renderer_timing_history",
     "crt_renderer_set_leaf_carry", "crt_renderer_set_xcd_regions", "crt_renderer_set_temporal_order",
     "crt_renderer_set_drain_threshold", "crt_renderer_set_wave_drain",
     "crt_renderer_attach_linear", "crt_renderer_set_kernel_variant", "crt_renderer_get_schedule_stats",
@@ -163,7 +163,7 @@ def hip():
             "crt_renderer_render": ([P, P, i32, i32, C.c_uint, P], i32),
             "crt_renderer_resolve": ([P, f32, P], i32), "crt_renderer_render_frame": ([P, P, P], i32),
             "crt_renderer_set_pixel_shard": ([P, i32, i32], i32),
-            "crt_renderer_synchronize": ([P, P], i32), "crt_renderer_last_timings": ([P, P], i32),
+            "crt_renderer_synchronize": ([P, P], i32), "crt_renderer_last_timings": ([P, P], i32), "crt_renderer_last_schedule": ([P, P], i32),
             "crt_renderer_timing_history": ([P, i32, P], i32),
             "crt_renderer_set_leaf_carry": ([P, i32, i32], i32),
             "crt_renderer_set_xcd_regions": ([P, i32], i32),

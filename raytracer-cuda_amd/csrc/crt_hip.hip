@@ -648,6 +648,11 @@ __device__ __forceinline__ void traverse_step(const float4* __restrict__ nodes, 
 // slot), then padding.  Slots [0, n_internal) are internal children at node first_child + slot; the
 // following slots are leaves whose primitives are consecutive from leaf_first in slot order; empty slots
 // have a zero-thickness box far away (never hit).
+// crt_render: variant 8 below 4 tiles per wave slot runs at occupancy 4 with the row prefetch when the probe's largest
+// tile work exceeds CRT_CHAIN_RHO times the mean work per occupancy-6 wave slot (a chain-bound frame), else at 6
+#ifndef CRT_CHAIN_RHO
+#define CRT_CHAIN_RHO 1.6   // profiles/r06y: occupancy 4 won at rho 1.62-6.4 and lost at 0.79-1.55 (one exception, -2 % at 1.54)
+#endif
 constexpr int STACK_LDS = 16;   // per-lane traversal-stack entries kept in LDS; deeper entries go to P.ovf
 #ifndef CRT_STACK6
 #define CRT_STACK6 12           // entries at occupancy 6 (6 one-wave workgroups per SIMD within 160 KiB: <= 6144 B each)
@@ -2443,8 +2448,11 @@ __global__ __launch_bounds__(1024) void crt_xcd_order_kernel(uint32_t* __restric
 // key_mode 1 adds the mean pixel (ties between tiles with equal maxima); key_mode 2 raises a tile to 3/4 of
 // the largest key among its 8 neighbours (a 4-spp probe underestimates some tiles next to expensive ones, and an
 // underestimated tile dispatched late becomes the launch's tail).
+// stats (optional, zeroed by the caller): [0] the largest tile work, [1] the sum of the tile works, both in probe cost units
+// over the probed pixels (a tile's work = the sum of its probed pixels' costs); the host's occupancy choice (crt_render)
 __global__ void crt_tile_cost_kernel(const uint32_t* __restrict__ pix_cost, int width, int height, int tiles_x,
-                                     int n_tiles, uint32_t* __restrict__ tile_cost, int key_mode, int stride) {
+                                     int n_tiles, uint32_t* __restrict__ tile_cost, int key_mode, int stride,
+                                     unsigned long long* __restrict__ stats) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tiles) return;
     const int x0 = (t % tiles_x) * 8, y0 = (t / tiles_x) * 8;
@@ -2457,6 +2465,10 @@ __global__ void crt_tile_cost_kernel(const uint32_t* __restrict__ pix_cost, int 
             ++k;
         }
     tile_cost[t] = key_mode == 1 ? m + sum / max(1u, k) : m;
+    if (stats) {
+        atomicMax(&stats[0], (unsigned long long)sum);
+        atomicAdd(&stats[1], (unsigned long long)sum);
+    }
 }
 __global__ void crt_tile_neighbour_kernel(const uint32_t* __restrict__ key_in, int tiles_x, int n_tiles,
                                           uint32_t* __restrict__ key_out) {
@@ -3081,6 +3093,9 @@ struct crt_renderer {
     uint32_t* d_tile_cost = nullptr;   // per-pixel probe costs
     uint32_t* d_order_hist = nullptr;
     uint32_t* d_tile_key = nullptr;    // variant 8: per-tile keys
+    unsigned long long* d_probe_stats = nullptr;   // crt_tile_cost_kernel's stats: largest tile work, total work
+    unsigned long long* h_probe_stats = nullptr;   // their pinned host copy
+    float last_schedule[4] = {0.f, 0.f, 0.f, 0.f};  // crt_renderer_last_schedule
     uint32_t* d_rng_cache = nullptr;   // curand_init result of (rng_cache_seed, rng_cache_base)
     unsigned long long rng_cache_seed = 0, rng_cache_base = 0;
     bool rng_cache_valid = false;
@@ -3492,6 +3507,8 @@ void crt_renderer_destroy(crt_renderer* R) {
     if (R->d_tile_cost) (void)hipFree(R->d_tile_cost);
     if (R->d_order_hist) (void)hipFree(R->d_order_hist);
     if (R->d_tile_key) (void)hipFree(R->d_tile_key);
+    if (R->d_probe_stats) (void)hipFree(R->d_probe_stats);
+    if (R->h_probe_stats) (void)hipHostFree(R->h_probe_stats);
     if (R->d_pix_rays) (void)hipFree(R->d_pix_rays);
     if (R->d_tile_order) (void)hipFree(R->d_tile_order);
     if (R->d_rng_cache) (void)hipFree(R->d_rng_cache);
@@ -3677,23 +3694,27 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     if (S->width != 4 && !(tv >= 0 && tv <= 3) && tv != 10) tv = probe_spp_for(R, spp) > 0 ? 10 : 3;
     // occupancy target (waves per SIMD): variant 8 runs at 7 (72 VGPRs, 8 LDS stack entries so that 28 one-wave
     // workgroups fit a CU's LDS; -2.4 % on config C, profiles/r03aj) when its frame has at least 4 tiles per wave slot,
-    // else at 6, or at 4 with the row prefetch when even 4 waves per SIMD leave fewer than 4.25 tiles per slot: a frame with
-    // few tiles per slot ends with its most expensive tiles' sequential sample chains (config B, 2 tiles per slot: +3.3 %
-    // at 7, profiles/r03ak), and the prefetch takes the node rows' wait off every iteration of a chain (B -8 % against
-    // occupancy 6, profiles/r06r, r06s, r06t; with more tiles the lost waves cost more: 1600x900 +18 %, C +24 %).  The
-    // other 4-wide variants run at 6, threaded scenes at 5.
+    // else at 6, or at 4 with the row prefetch when the cost probe shows a chain-bound frame: a frame with few tiles per
+    // slot can end with its most expensive tiles' sequential sample chains (config B, 2 tiles per slot: +3.3 % at 7,
+    // profiles/r03ak), and the prefetch takes the node rows' wait off every iteration of a chain (B -8 % against
+    // occupancy 6, profiles/r06r-r06u; where the frame is not chain-bound the lost waves cost more: the plain Cornell box
+    // at 1280x720 +15 %, 1600x900 +17 %, C +24 %; profiles/r06y).  The other 4-wide variants run at 6, threaded scenes
+    // at 5.
     // Variants 10 and 3 (threaded, bit-exact) run at 6 (80 VGPRs; -8.0 % and -4.8 % against 5, profiles/r03am, r03as).
     int occ = R->min_waves ? R->min_waves : (S->width == 4 || tv == 10 || tv == 3 ? 6 : 5);
+    bool auto_small = false;   // variant 8, automatic occupancy, few tiles per slot: 4 or 6 from the probe's statistics
+    R->last_schedule[0] = R->last_schedule[1] = R->last_schedule[2] = R->last_schedule[3] = 0.f;
     if (!R->min_waves && S->width == 4 && (wv == 8 || R->tile_shards > 1)) {
         if (!R->n_cus) HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
         const size_t tiles = (size_t)((R->width + 7) / 8) * ((R->height + 7) / 8) / (size_t)std::max(1, R->tile_shards);
-        // at least 4 tiles per wave slot: occupancy 7 (throughput); fewer than 4.25 per slot even at occupancy 4: the
-        // frame ends with its most expensive tiles' sample chains, which the row prefetch of occupancy 4 shortens (at 256
-        // spp, against occupancy 6: 3.5 tiles per slot (config B) -8 %, 3.9 -7 %, 4.0 -6 %, 4.5 +2 %, 5.5 +18 %; a
-        // 2000-spp pixel shard at 1.8 per slot -6.5 %; profiles/r06t, r06u); in between, 6.  (The counting kernel keeps
-        // 6: its counts do not depend on the schedule.)
+        // at least 4 tiles per wave slot: occupancy 7 (throughput).  Fewer: 4 or 6.  With the cost probe the probe's
+        // tile works decide (below, after the sort); without it, fewer than 4.25 tiles per occupancy-4 slot take 4 (the
+        // crossover of the bunny scene at 256 spp, profiles/r06t, r06u).  (The counting kernel keeps 6: its counts do not
+        // depend on the schedule.)
         const size_t slots4 = (size_t)4 * R->n_cus * 4;
         occ = tiles >= (size_t)4 * R->n_cus * 4 * 7 ? 7 : (4 * tiles < 17 * slots4 && !cnt) ? 4 : 6;
+        // below 4 tiles per slot and with the cost probe, the probe's tile works decide between 4 and 6 (below)
+        if (occ < 7 && !cnt && probe_spp_for(R, spp) > 0) occ = 6, auto_small = true;
     }
     P.stack_lds = std::min(R->stack_lds, occ >= 7 ? CRT_STACK7 : occ >= 6 ? CRT_STACK6 : STACK_LDS);
     // a stack_cap override below the LDS entries must still report the entries it drops (crt_scene_options.stack_cap)
@@ -3744,8 +3765,18 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             const dim3 pgrid((R->width + ps - 1) / ps, (R->height + ps - 1) / ps);
             if (occ >= 6) hipLaunchKernelGGL((crt_render_kernel<true, 4, 6>), pgrid, block, 0, st, Q);
             else hipLaunchKernelGGL((crt_render_kernel<true, 4, 5>), pgrid, block, 0, st, Q);
+            if (auto_small) {
+                if (!R->d_probe_stats) {
+                    HIP_TRY(hipMalloc((void**)&R->d_probe_stats, 2 * sizeof(unsigned long long)));
+                    HIP_TRY(hipHostMalloc((void**)&R->h_probe_stats, 2 * sizeof(unsigned long long)));
+                }
+                HIP_TRY(hipMemsetAsync(R->d_probe_stats, 0, 2 * sizeof(unsigned long long), st));
+            }
             hipLaunchKernelGGL(crt_tile_cost_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_tile_cost,
-                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode, pst);
+                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode, pst,
+                               auto_small ? R->d_probe_stats : nullptr);
+            if (auto_small) HIP_TRY(hipMemcpyAsync(R->h_probe_stats, R->d_probe_stats, 2 * sizeof(unsigned long long),
+                                                   hipMemcpyDeviceToHost, st));
             if (R->tile_key_mode == 2) {   // per-pixel costs are no longer needed: reuse them for the smoothed keys
                 hipLaunchKernelGGL(crt_tile_neighbour_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st,
                                    R->d_tile_key, tiles_x, n_tiles, R->d_tile_cost);
@@ -3767,6 +3798,26 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             P.order = R->d_order;
             P.crit_tiles = R->crit_tiles < 0 ? 4 * R->n_cus : R->crit_tiles;
             P.crit_threshold = R->crit_threshold;
+            if (auto_small) {
+                // Chain-bound or not, from the probe's tile works: rho = the largest tile's work over the mean work per
+                // wave slot at occupancy 6 (this rank's share of the tiles when pixel-sharded).  rho > 1 means the most
+                // expensive tile alone outlasts an even spread of the frame over the slots; above CRT_CHAIN_RHO the frame
+                // runs at occupancy 4 with the row prefetch, which shortens every chain iteration (-9 %) and gives up a
+                // third of the wave slots (profiles/r06x, r06y: config B rho 2.0, -7.6 %; the plain Cornell box at the
+                // same size rho 0.8, +15 % at 4).  One host synchronisation after the sort.
+                HIP_TRY(hipStreamSynchronize(st));
+                const double mx = (double)R->h_probe_stats[0];
+                const double mine = (double)R->h_probe_stats[1] / std::max(1, R->tile_shards);
+                const double rho = mine > 0 ? mx * (4.0 * R->n_cus * 6) / mine : 0.0;
+                if (rho > CRT_CHAIN_RHO) {
+                    occ = 4;
+                    P.stack_lds = std::min(R->stack_lds, STACK_LDS);
+                    if (S->stack_cap > 0) P.stack_lds = std::min(P.stack_lds, S->stack_cap);
+                }
+                R->last_schedule[0] = (float)rho;
+                R->last_schedule[2] = (float)mx;
+                R->last_schedule[3] = (float)(mine / std::max(1, n_tiles / std::max(1, R->tile_shards)));
+            }
         }
         if (R->tile_shards > 1 && !P.order) {   // pixel shard without the probe: this shard's tiles in row order
             hipLaunchKernelGGL(crt_shard_tiles_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_order, n_tiles,
@@ -3775,6 +3826,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
         }
         if (P.crit_tiles > 0) P.crit_tiles = (P.crit_tiles + R->tile_shards - 1) / R->tile_shards;
         const dim3 tgrid((unsigned)((n_tiles - R->tile_shard + R->tile_shards - 1) / R->tile_shards)), tblock(64);
+        R->last_schedule[1] = (float)occ;
         const char* cs = cnt ? "true" : "false";
         HIP_TRY(hipEventRecord(R->ev_main, st));
         if (occ >= 7) {
@@ -3836,7 +3888,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
                 // first, so the long paths start early and the launch does not end with them (profiles/r04i: a 1-spp
                 // frame in row order spends its last 31 % draining)
                 hipLaunchKernelGGL(crt_tile_cost_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_pix_rays,
-                                   R->width, R->height, tiles_x, n_tiles, R->d_tile_order, 0, 1);
+                                   R->width, R->height, tiles_x, n_tiles, R->d_tile_order, 0, 1, nullptr);
                 hipLaunchKernelGGL(crt_tile_neighbour_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st,
                                    R->d_tile_order, tiles_x, n_tiles, R->d_tile_key);
                 const unsigned ob = (unsigned)((n_tiles + ORDER_ITEMS - 1) / ORDER_ITEMS);
@@ -3910,7 +3962,7 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
             Q.probe_cost = R->d_tile_cost;
             hipLaunchKernelGGL((crt_render_kernel<true, 3, 5>), grid, block, 0, st, Q);
             hipLaunchKernelGGL(crt_tile_cost_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st, R->d_tile_cost,
-                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode, 1);
+                               R->width, R->height, tiles_x, n_tiles, R->d_tile_key, R->tile_key_mode, 1, nullptr);
             if (R->tile_key_mode == 2) {
                 hipLaunchKernelGGL(crt_tile_neighbour_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, st,
                                    R->d_tile_key, tiles_x, n_tiles, R->d_tile_cost);
@@ -4231,6 +4283,12 @@ int crt_renderer_set_leaf_carry(crt_renderer* R, int lanes, int max_pairs) {
     (void)max_pairs;
     return set_error(CRT_ERR_UNSUPPORTED, "leaf-pair carry: not in this build (measured and removed, DESIGN.md §8; "
                                           "profiles/r04c/leaf_carry.patch)");
+}
+
+int crt_renderer_last_schedule(crt_renderer* R, float out[4]) {
+    if (!R || !out) return set_error(CRT_ERR_INVALID_ARGUMENT, "null argument");
+    for (int k = 0; k < 4; ++k) out[k] = R->last_schedule[k];
+    return CRT_OK;
 }
 
 int crt_renderer_last_timings(crt_renderer* R, float out[3]) {

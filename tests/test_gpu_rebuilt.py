@@ -288,6 +288,24 @@ def test_occupancy_seven_is_bit_identical_and_automatic(rebuilt):
     assert small.last_kernel_name() == "crt_render_kernel<false, 8, 4>"
 
 
+def test_occupancy_choice_follows_the_probe(rebuilt):
+    """Below 4 tiles per wave slot the cost probe decides between occupancy 4 (row prefetch) and 6: config B's frame
+    (the glass bunny's tiles outlast an even spread of the frame over the wave slots: rho = largest tile work / mean work
+    per slot ~ 2) runs at 4, the plain Cornell box at the same size (rho ~ 0.8) at 6; last_schedule reports the choice."""
+    got = {}
+    for scene in ("cornell_bunny", "cornell"):
+        r = crt_amd.Renderer(1280, 720)
+        r.set_camera(crt_amd.camera(64))
+        r.init_rand(41)
+        r.render(rebuilt[scene, "w4"], 64, 20)
+        r.synchronize()
+        got[scene] = (r.last_kernel_name(), r.last_schedule())
+    (kb, sb), (kc, sc) = got["cornell_bunny"], got["cornell"]
+    assert kb == "crt_render_kernel<false, 8, 4>" and sb["occupancy"] == 4 and sb["rho"] > 1.6, sb
+    assert kc == "crt_render_kernel<false, 8, 6>" and sc["occupancy"] == 6 and 0 < sc["rho"] < 1.6, sc
+    assert sb["max_tile_work"] > sb["mean_tile_work"] > 0
+
+
 @pytest.mark.parametrize("scene,w,h,spp", [("cornell_bunny", 100, 37, 70), ("cornell_bunny", 1280, 720, 64),
                                            ("cornell_1m", 320, 180, 64)])
 def test_row_prefetch_is_bit_identical(rebuilt, request, scene, w, h, spp):

@@ -44,5 +44,6 @@ for rnd in range(a.rounds):
             if k:
                 ms.append(r.last_kernel_ms())
         print(json.dumps({"round": rnd, "w": a.w, "h": a.h, "spp": a.spp, "pixel_shard": a.pixel_shard, "tiles": tiles,
-                          "occupancy": occ, "kernel": r.last_kernel_name(), "main_kernel_ms": round(sum(ms) / len(ms), 3)}),
+                          "occupancy": occ, "kernel": r.last_kernel_name(), "main_kernel_ms": round(sum(ms) / len(ms), 3),
+                          "schedule": r.last_schedule()}),
               flush=True)
