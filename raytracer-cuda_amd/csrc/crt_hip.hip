@@ -3707,14 +3707,12 @@ int crt_renderer_render(crt_renderer* R, const crt_scene* S, int spp, int max_bo
     if (!R->min_waves && S->width == 4 && (wv == 8 || R->tile_shards > 1)) {
         if (!R->n_cus) HIP_TRY(hipDeviceGetAttribute(&R->n_cus, hipDeviceAttributeMultiprocessorCount, R->device));
         const size_t tiles = (size_t)((R->width + 7) / 8) * ((R->height + 7) / 8) / (size_t)std::max(1, R->tile_shards);
-        // at least 4 tiles per wave slot: occupancy 7 (throughput).  Fewer: 4 or 6.  With the cost probe the probe's
-        // tile works decide (below, after the sort); without it, fewer than 4.25 tiles per occupancy-4 slot take 4 (the
-        // crossover of the bunny scene at 256 spp, profiles/r06t, r06u).  (The counting kernel keeps 6: its counts do not
-        // depend on the schedule.)
-        const size_t slots4 = (size_t)4 * R->n_cus * 4;
-        occ = tiles >= (size_t)4 * R->n_cus * 4 * 7 ? 7 : (4 * tiles < 17 * slots4 && !cnt) ? 4 : 6;
-        // below 4 tiles per slot and with the cost probe, the probe's tile works decide between 4 and 6 (below)
-        if (occ < 7 && !cnt && probe_spp_for(R, spp) > 0) occ = 6, auto_small = true;
+        // at least 4 tiles per wave slot: occupancy 7 (throughput).  Fewer: 6, or 4 when the cost probe's tile works
+        // show a chain-bound frame (decided after the sort, below; without the probe there is nothing to decide on,
+        // and the tile count alone cannot tell: at 1280x720 the bunny gains 8 % at 4 and the plain Cornell box loses
+        // 16 %, profiles/r06x).  (The counting kernel keeps 6: its counts do not depend on the schedule.)
+        occ = tiles >= (size_t)4 * R->n_cus * 4 * 7 ? 7 : 6;
+        if (occ < 7 && !cnt && probe_spp_for(R, spp) > 0) auto_small = true;
     }
     P.stack_lds = std::min(R->stack_lds, occ >= 7 ? CRT_STACK7 : occ >= 6 ? CRT_STACK6 : STACK_LDS);
     // a stack_cap override below the LDS entries must still report the entries it drops (crt_scene_options.stack_cap)
