@@ -306,17 +306,20 @@ def test_occupancy_choice_follows_the_probe(rebuilt):
     assert sb["max_tile_work"] > sb["mean_tile_work"] > 0
 
 
-@pytest.mark.parametrize("scene,w,h,spp", [("cornell_bunny", 100, 37, 70), ("cornell_bunny", 1280, 720, 64),
-                                           ("cornell_1m", 320, 180, 64)])
-def test_row_prefetch_is_bit_identical(rebuilt, request, scene, w, h, spp):
+@pytest.mark.parametrize("scene,w,h,spp,stack", [("cornell_bunny", 100, 37, 70, 0), ("cornell_bunny", 1280, 720, 64, 0),
+                                                 ("cornell_1m", 320, 180, 64, 0), ("cornell_bunny", 160, 90, 64, 1)])
+def test_row_prefetch_is_bit_identical(rebuilt, request, scene, w, h, spp, stack):
     """Variant 8 at occupancy 4 loads each lane's next node rows during the step's first leaf round and uses them in the
     next node step (lanes given a new ray in between load their own): frames, RNG state and ray counts equal occupancy
-    6's, on a ragged frame, a config-B-sized frame and the deep 1M-triangle tree."""
+    6's, on a ragged frame, a config-B-sized frame, the deep 1M-triangle tree and with one LDS stack entry (every
+    deeper entry pushed to and popped from the HBM overflow region)."""
     dev = request.getfixturevalue("config_e")[0] if scene == "cornell_1m" else rebuilt[scene, "w4"]
     out = []
     for occ in (6, 4):
         r = crt_amd.Renderer(w, h)
         r.set_occupancy_target(occ)
+        if stack:
+            r.set_stack_lds(stack)
         r.set_camera(crt_amd.camera(spp))
         r.init_rand(41)
         r.render(dev, spp, 20)
