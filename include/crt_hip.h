@@ -300,9 +300,12 @@ int  crt_renderer_set_pixel_shard(crt_renderer* r, int shard, int shards);
  * per-pixel region in HBM.  Results do not depend on it (tests force the HBM path with 1). */
 int  crt_renderer_set_stack_lds(crt_renderer* r, int entries);
 /* Register-allocation occupancy target in waves per SIMD (1 = compiler default, 4-8; 0 = auto, the default: 7 for
- * variant 8 when the frame has at least 4 of its 8x8 tiles per wave slot, 6 for the other 4-wide launches and for
- * variants 3 and 10, 5 for variants 0-2).  The 4-wide kernels keep 12 traversal-stack
- * entries per lane in LDS at 6 waves and 8 at 7+ (LDS is allocated in 1-KiB steps per workgroup). */
+ * variant 8 when the frame has at least 4 of its 8x8 tiles per wave slot; below that, 4 when the cost probe finds the
+ * frame chain-bound (its largest tile work over the mean work per occupancy-6 wave slot above 1.6; the host then waits
+ * for the probe and the tile sort before launching the main kernel) and 6 otherwise; 6 for the other 4-wide launches
+ * and for variants 3 and 10, 5 for variants 0-2).  Variant 8 at 4 loads each lane's next node rows during the leaf
+ * round (crt_render_kernel<false, 8, 4>).  The 4-wide kernels keep 16 traversal-stack entries per lane in LDS at 4-5
+ * waves, 12 at 6 and 8 at 7+ (LDS is allocated in 1-KiB steps per workgroup). */
 int  crt_renderer_set_occupancy_target(crt_renderer* r, int waves_per_simd);
 /* Trace `spp` samples per pixel continuing each pixel's RNG stream; the per-pixel
  * linear sum (pixel_color, CUDAKernels.h:157-162) is kept in an fp32 W*H*3 buffer. */
