@@ -557,6 +557,10 @@ def run(args) -> int:
     dist_t = gather_frame_timings(fr) if grouped else None
     rays_rank = r.counters()["rays"]
     kname = r.last_kernel_name()      # the instantiation the timed frames ran (rocprofv3's spelling)
+    try:                              # the occupancy choice behind it (crt_renderer_last_schedule; absent in old builds)
+        schedule = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.last_schedule().items()}
+    except (AttributeError, crt.CrtError if hasattr(crt, "CrtError") else AttributeError):
+        schedule = None
     phases = r.last_timings()         # the last timed frame: probe + tile sort, and the main render kernel alone
     # every timed frame's phases (the renderer keeps the last 32 frames' HIP events): the roofline divides by the
     # main kernel's average over the timed frames, the same quantity rocprofv3's average duration measures.  A base
@@ -713,6 +717,7 @@ def run(args) -> int:
             "frame_wall_s": round(ms_per_step / 1e3, 4),
             "rays_per_frame": rays_frame,
             "paths_per_s": round(W * H * args.spp * args.steps / elapsed, 1),
+            "render_kernel": kname, "render_schedule": schedule,
             "render_kernel_ms_avg": round(kernel_ms_avg, 3), "render_kernel_ms_max_over_ranks": round(kernel_ms_max, 3),
             "render_phases_ms_last_frame": {k: round(v, 3) for k, v in phases.items()},
             "render_phases_ms_avg": {k: round(v, 3) for k, v in phases_avg.items()},
