@@ -557,9 +557,11 @@ def run(args) -> int:
     dist_t = gather_frame_timings(fr) if grouped else None
     rays_rank = r.counters()["rays"]
     kname = r.last_kernel_name()      # the instantiation the timed frames ran (rocprofv3's spelling)
-    try:                              # the occupancy choice behind it (crt_renderer_last_schedule; absent in old builds)
+    # the occupancy choice behind it (crt_renderer_last_schedule); None for the CPU rig and for builds without it
+    schedule_errors = (AttributeError,) + ((crt.CrtError,) if hasattr(crt, "CrtError") else ())
+    try:
         schedule = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.last_schedule().items()}
-    except (AttributeError, crt.CrtError if hasattr(crt, "CrtError") else AttributeError):
+    except schedule_errors:
         schedule = None
     phases = r.last_timings()         # the last timed frame: probe + tile sort, and the main render kernel alone
     # every timed frame's phases (the renderer keeps the last 32 frames' HIP events): the roofline divides by the
